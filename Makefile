@@ -1,0 +1,40 @@
+# Builds the product library (HIP kernels + C ABI) for gfx950, in-tree, and the
+# CPU oracle (test infrastructure).  `python -c "import __graft_entry__ as g; g.build()"`
+# runs this.
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+CXXFLAGS ?= -O3 -fPIC -std=c++17 -Wall -Wextra
+PKG      := rustnetworkstack_amd
+CSRC     := $(PKG)/csrc
+BUILD    := $(PKG)/build
+LIB      := $(PKG)/librns_checksum.so
+
+all: $(LIB) oracle
+
+$(BUILD)/rns_checksum.o: $(CSRC)/rns_checksum.hip include/rns_checksum.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -Iinclude -c $< -o $@
+
+$(BUILD)/host_checksum.o: $(CSRC)/host_checksum.cpp include/rns_checksum.h
+	@mkdir -p $(BUILD)
+	g++ $(CXXFLAGS) -Iinclude -c $< -o $@
+
+$(LIB): $(BUILD)/rns_checksum.o $(BUILD)/host_checksum.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
+
+oracle:
+	$(MAKE) -C oracle
+
+# Register / occupancy report for every kernel instantiation.
+resources: $(CSRC)/rns_checksum.hip
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -Iinclude -c $< -o /dev/null -Rpass-analysis=kernel-resource-usage
+
+asm: $(CSRC)/rns_checksum.hip
+	@mkdir -p $(BUILD)/asm
+	cd $(BUILD)/asm && $(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -I../../../include -c ../../../$< -o rns.o -save-temps
+
+clean:
+	rm -rf $(BUILD) $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle resources asm clean

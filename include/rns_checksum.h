@@ -1,0 +1,157 @@
+/*
+ * rns_checksum.h — C ABI of the MI355X-native Internet checksum path.
+ *
+ * Drop-in boundary for jbush001/RustNetworkStack's checksum core
+ * (src/stack/util.rs:86-119, 180-207).  The reference binds native code with
+ * `#[repr(C)]` structs and `extern "C"` functions returning int
+ * (src/stack/netif.rs:24-37, built by build.rs:19-21); this header follows the
+ * same convention: plain pointers and sizes, no HIP or torch types, status
+ * codes instead of exceptions.  INTEGRATION.md shows the Rust `extern "C"`
+ * block and build.rs lines a maintainer would add.
+ *
+ * Two groups of entry points:
+ *
+ *  1. Per-packet host calls with the reference's exact signatures and results.
+ *     They run on the calling CPU thread (a GPU launch costs microseconds; one
+ *     packet costs ~100 ns), are re-entrant, and are what util.rs's four
+ *     functions forward to.  Where the reference panics they return a negative
+ *     status; the Rust shim turns that back into the same panic.
+ *
+ *  2. Batch calls that run the hand-written gfx950 kernels over many packets at
+ *     once: device-resident (descriptors + arena already in HBM) and
+ *     host-resident (pinned staging, overlapped copies).  They never fall back
+ *     to the CPU: without a usable GPU they return RNS_E_NODEVICE.
+ *
+ * Result semantics (both groups, bit-exact with util.rs:88-106): the value is
+ * the reference's u32 accumulator — seed + sum of big-endian 16-bit words, an
+ * odd final byte counted as (byte << 8), wrapping mod 2^32 like a release
+ * build — folded end-around to 16 bits.  RNS_FLAG_COMPLEMENT XORs it with
+ * 0xffff, which is what every call site stores or tests (ip.rs:76,158;
+ * tcp.rs:848,970; udp.rs:168; icmp.rs:46,71,91,110).
+ */
+#ifndef RNS_CHECKSUM_H
+#define RNS_CHECKSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RNS_ABI_VERSION 1
+
+/* ---- status codes (0 = ok, < 0 = error; never abort) ------------------- */
+#define RNS_OK            0
+#define RNS_E_INVALID    (-1)  /* bad argument (NULL pointer, bad address length, ...)  */
+#define RNS_E_EMPTY      (-2)  /* empty slice: the reference panics (util.rs:92)           */
+#define RNS_E_BOUNDS     (-3)  /* a packet descriptor lies outside its arena               */
+#define RNS_E_NODEVICE   (-4)  /* no usable gfx950 device / HIP runtime                     */
+#define RNS_E_ORDER      (-5)  /* host batch: offsets not ascending                         */
+#define RNS_E_TOOLARGE   (-6)  /* host batch: one packet larger than the staging chunk      */
+#define RNS_E_HIP_BASE   (-1000) /* RNS_E_HIP_BASE - hipError_t: HIP runtime error          */
+
+/* ---- flags for batch calls ---------------------------------------------- */
+#define RNS_FLAG_COMPLEMENT 0x1u   /* store 0xffff ^ sum (the transmitted / verified value) */
+
+/* Fragment of a packet, same layout as the reference's `#[repr(C)] struct IOVec
+ * { base: *const u8, len: usize }` (netif.rs:24-29). */
+typedef struct rns_iovec {
+    const uint8_t *base;
+    size_t len;
+} rns_iovec;
+
+/* IP address, the C form of `enum IPAddr { V4([u8;4]), V6([u8;16]) }`
+ * (util.rs:22-26): version is 4 or 6; V4 uses bytes[0..4]. */
+typedef struct rns_ipaddr {
+    uint32_t version;
+    uint8_t bytes[16];
+} rns_ipaddr;
+
+/* ========================================================================
+ * 1. Per-packet host calls (util.rs)
+ * ====================================================================== */
+
+/* util.rs:88 `pub fn compute_ones_comp(in_checksum: u16, slice: &[u8]) -> u16`.
+ * Returns the 16-bit sum (>= 0), or RNS_E_EMPTY for len == 0 / RNS_E_INVALID. */
+int32_t rns_compute_ones_comp(uint16_t in_checksum, const uint8_t *slice, size_t len);
+
+/* util.rs:108 `pub fn compute_checksum(slice: &[u8]) -> u16` = 0xffff ^ ones_comp(0, slice). */
+int32_t rns_compute_checksum(const uint8_t *slice, size_t len);
+
+/* util.rs:112 `pub fn compute_buffer_ones_comp(initial_sum: u16, buffer: &NetBuffer) -> u16`.
+ * `frags` are the slices NetBuffer::iter yields (buf.rs:466-487), folded one at
+ * a time, so an odd-length non-final fragment is zero-padded like the reference.
+ * An empty fragment returns RNS_E_EMPTY (the reference would panic on it). */
+int32_t rns_compute_buffer_ones_comp(uint16_t initial_sum, const rns_iovec *frags, size_t nfrags);
+
+/* util.rs:180 `pub fn compute_pseudo_header_checksum(source_ip, dest_ip, length: usize,
+ * protocol: u8) -> u16`.  Layout follows dest_ip's version (util.rs:186); a
+ * source of the other version is RNS_E_INVALID (the reference panics in copy_to). */
+int32_t rns_compute_pseudo_header_checksum(const rns_ipaddr *source_ip, const rns_ipaddr *dest_ip,
+                                           uint64_t length, uint8_t protocol);
+
+/* ========================================================================
+ * 2. Batch calls (HIP kernels for gfx950)
+ * ====================================================================== */
+
+/* Device-resident batch.  All pointers are device pointers on the current HIP
+ * device; `stream` is a hipStream_t (NULL = the null stream).  Packet i is the
+ * bytes d_arena[d_off[i] .. d_off[i] + d_len[i]) at any byte alignment; its seed
+ * is d_seed[i] (d_seed == NULL => 0).  d_out[i] receives the result.
+ * A descriptor outside [0, arena_bytes) gets d_out[i] = 0 and is counted in
+ * *d_bad (device u32, optional, not reset by the call).  len == 0 gives the seed
+ * (the reference panics).  `len_hint` is the typical packet
+ * length in bytes (0 = unknown): it only picks the lanes-per-packet shape.
+ * Asynchronous: returns after the launch; errors of the launch itself are
+ * returned, never raised. */
+int rns_csum_batch_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off,
+                       const uint32_t *d_len, const uint16_t *d_seed, uint16_t *d_out, uint32_t n,
+                       uint32_t flags, uint32_t len_hint, uint32_t *d_bad, void *stream);
+
+/* Same, for packets at a fixed stride (no offset/length arrays to read):
+ * packet i = d_arena[first_off + i*stride .. + len). */
+int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uint64_t first_off,
+                               uint64_t stride, uint32_t len, const uint16_t *d_seed, uint16_t *d_out,
+                               uint32_t n, uint32_t flags, uint32_t *d_bad, void *stream);
+
+/* Tuning entry (bench / tests): explicit shape.  lanes_per_packet in
+ * {4,8,16,32,64}, unroll in {1,2,4}, max_blocks = grid cap (0 = one packet group
+ * per thread group, no grid-stride loop). */
+int rns_csum_batch_dev_cfg(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off,
+                           const uint32_t *d_len, const uint16_t *d_seed, uint16_t *d_out, uint32_t n,
+                           uint32_t flags, uint32_t lanes_per_packet, uint32_t unroll,
+                           uint32_t max_blocks, uint32_t *d_bad, void *stream);
+
+/* Host-resident batch through a staging context: chunked H2D copies, kernels and
+ * D2H copies of the 2-byte results overlapped on several streams of `device`.
+ * Offsets must be ascending.  Synchronous (returns when h_out is filled).
+ * For full PCIe rate allocate h_arena with rns_host_alloc (pinned).  A context
+ * serialises its own calls (internal mutex); use one per thread for concurrency. */
+typedef struct rns_host_ctx rns_host_ctx;
+int rns_host_ctx_create(int device, uint64_t chunk_bytes, uint32_t nstreams, rns_host_ctx **out);
+int rns_host_ctx_destroy(rns_host_ctx *ctx);
+int rns_csum_batch_host(rns_host_ctx *ctx, const uint8_t *h_arena, uint64_t arena_bytes,
+                        const uint64_t *h_off, const uint32_t *h_len, const uint16_t *h_seed,
+                        uint16_t *h_out, uint32_t n, uint32_t flags);
+
+/* Pinned host memory for arenas handed to rns_csum_batch_host. */
+int rns_host_alloc(uint64_t bytes, void **out);
+int rns_host_free(void *p);
+
+/* Deterministic synthetic packet bytes on the device: splitmix64 stream,
+ * little-endian words, word i = mix(seed + (i+1)*0x9E3779B97F4A7C15) — the
+ * generator oracle/oracle.py splitmix64_bytes restates on the CPU. */
+int rns_fill_splitmix64_dev(uint8_t *d_buf, uint64_t nbytes, uint64_t seed, void *stream);
+
+/* ---- introspection ------------------------------------------------------- */
+int rns_abi_version(void);
+const char *rns_strerror(int status);
+const char *rns_build_info(void);
+int rns_device_count(void);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* RNS_CHECKSUM_H */

@@ -1,0 +1,207 @@
+"""ORACLE — test infrastructure only.
+
+Python access to the CPU restatement of jbush001/RustNetworkStack's checksum
+path (src/stack/util.rs:88-119, 180-207):
+
+* ``ones_comp_py`` etc. — pure-Python literal loops, for tiny inputs and for
+  cross-checking the C restatement;
+* ``Oracle`` — ctypes binding of ``oracle/build/libcsum_oracle.so`` (the C
+  restatement in csum_oracle.c), fast enough for full-size batches.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+Panics of the reference are raised as ``ReferencePanic``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libcsum_oracle.so")
+
+
+class ReferencePanic(Exception):
+    """The reference would panic here (e.g. util.rs:92 on an empty slice)."""
+
+
+# --------------------------------------------------------------------------
+# pure-Python literal restatement (small inputs only)
+# --------------------------------------------------------------------------
+def ones_comp_py(in_checksum: int, data: bytes) -> int:
+    """util.rs:88-106, literally (u32 accumulator, BE words, odd byte << 8)."""
+    if len(data) == 0:
+        raise ReferencePanic("compute_ones_comp on empty slice (util.rs:92)")
+    checksum = in_checksum & 0xFFFF
+    i = 0
+    while i < len(data) - 1:
+        checksum = (checksum + ((data[i] << 8) | data[i + 1])) & 0xFFFFFFFF
+        i += 2
+    if i < len(data):
+        checksum = (checksum + (data[i] << 8)) & 0xFFFFFFFF
+    while checksum > 0xFFFF:
+        checksum = (checksum & 0xFFFF) + (checksum >> 16)
+    return checksum
+
+
+def checksum_py(data: bytes) -> int:
+    """util.rs:108-110."""
+    return 0xFFFF ^ ones_comp_py(0, data)
+
+
+def buffer_ones_comp_py(initial_sum: int, fragments) -> int:
+    """util.rs:112-119 over the fragment slices buf.rs:466-487 yields."""
+    s = initial_sum
+    for frag in fragments:
+        s = ones_comp_py(s, bytes(frag))
+    return s
+
+
+def pseudo_header_py(src: bytes, dst: bytes, length: int, protocol: int) -> int:
+    """util.rs:180-207 (layout chosen by the dest variant, util.rs:186)."""
+    if len(src) not in (4, 16) or len(dst) not in (4, 16) or len(src) != len(dst):
+        raise ReferencePanic("IPAddr variant/length mismatch (util.rs:41-56)")
+    if len(dst) == 4:
+        ph = bytearray(12)
+        ph[0:4] = src
+        ph[4:8] = dst
+        ph[9] = protocol & 0xFF
+        ph[10:12] = (length & 0xFFFF).to_bytes(2, "big")
+    else:
+        ph = bytearray(40)
+        ph[0:16] = src
+        ph[16:32] = dst
+        ph[32:36] = (length & 0xFFFFFFFF).to_bytes(4, "big")
+        ph[39] = protocol & 0xFF
+    return ones_comp_py(0, bytes(ph))
+
+
+# --------------------------------------------------------------------------
+# deterministic synthetic bytes: splitmix64 (seed 0x5EED_C0DE)
+# --------------------------------------------------------------------------
+GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+
+
+def splitmix64_words(seed: int, count: int, start: int = 0) -> np.ndarray:
+    """Words z_i = mix(seed + (start+i+1)*GOLDEN), i in [0, count)."""
+    with np.errstate(over="ignore"):
+        idx = np.arange(start + 1, start + count + 1, dtype=np.uint64)
+        z = np.uint64(seed) + idx * GOLDEN
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z
+
+
+def splitmix64_bytes(seed: int, nbytes: int) -> np.ndarray:
+    """Little-endian byte stream of splitmix64 words (uint8 array of nbytes)."""
+    words = splitmix64_words(seed, (nbytes + 7) // 8)
+    return words.view(np.uint8)[:nbytes].copy()
+
+
+# --------------------------------------------------------------------------
+# ctypes binding of the C restatement
+# --------------------------------------------------------------------------
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", HERE])
+    return LIB_PATH
+
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+def _ptr(a: np.ndarray, ctype=ctypes.c_uint8):
+    return a.ctypes.data_as(ctypes.POINTER(ctype))
+
+
+class Oracle:
+    """ctypes view of oracle/csum_oracle.c."""
+
+    def __init__(self, path: str | None = None):
+        self.lib = ctypes.CDLL(path or build())
+        L = self.lib
+        L.oracle_compute_ones_comp.restype = ctypes.c_int32
+        L.oracle_compute_ones_comp.argtypes = [ctypes.c_uint16, ctypes.c_void_p, ctypes.c_size_t]
+        L.oracle_compute_checksum.restype = ctypes.c_int32
+        L.oracle_compute_checksum.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        L.oracle_compute_buffer_ones_comp.restype = ctypes.c_int32
+        L.oracle_compute_buffer_ones_comp.argtypes = [
+            ctypes.c_uint16, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t]
+        L.oracle_compute_pseudo_header_checksum.restype = ctypes.c_int32
+        L.oracle_compute_pseudo_header_checksum.argtypes = [
+            ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint8]
+        L.oracle_batch.restype = None
+        L.oracle_batch.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_int]
+        L.oracle_batch_mt.restype = ctypes.c_int
+        L.oracle_batch_mt.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
+        L.oracle_time_ones_comp.restype = ctypes.c_double
+        L.oracle_time_ones_comp.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]
+
+    @staticmethod
+    def _check(r: int) -> int:
+        if r < 0:
+            raise ReferencePanic("reference would panic")
+        return r
+
+    def compute_ones_comp(self, in_checksum: int, data) -> int:
+        b = bytes(data)
+        return self._check(self.lib.oracle_compute_ones_comp(in_checksum & 0xFFFF, b, len(b)))
+
+    def compute_checksum(self, data) -> int:
+        b = bytes(data)
+        return self._check(self.lib.oracle_compute_checksum(b, len(b)))
+
+    def compute_buffer_ones_comp(self, initial_sum: int, fragments) -> int:
+        frags = [bytes(f) for f in fragments]
+        n = len(frags)
+        bufs = [ctypes.create_string_buffer(f, len(f) or 1) for f in frags]
+        bases = (ctypes.c_void_p * max(n, 1))(*[ctypes.cast(b, ctypes.c_void_p).value for b in bufs])
+        lens = (ctypes.c_size_t * max(n, 1))(*[len(f) for f in frags])
+        return self._check(self.lib.oracle_compute_buffer_ones_comp(initial_sum & 0xFFFF, bases, lens, n))
+
+    def compute_pseudo_header_checksum(self, src: bytes, dst: bytes, length: int, protocol: int) -> int:
+        return self._check(self.lib.oracle_compute_pseudo_header_checksum(
+            bytes(src), len(src), bytes(dst), len(dst), length & 0xFFFFFFFFFFFFFFFF, protocol & 0xFF))
+
+    def batch(self, arena: np.ndarray, off: np.ndarray, length: np.ndarray, seed: np.ndarray | None,
+              complement: bool = False, threads: int = 1) -> np.ndarray:
+        """One compute_ones_comp per packet (optionally complemented)."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        n = off.shape[0]
+        if n and int((off + length.astype(np.uint64)).max()) > arena.shape[0]:
+            raise ValueError("descriptor out of arena bounds")
+        out = np.empty(n, dtype=np.uint16)
+        sp = None
+        if seed is not None:
+            seed = np.ascontiguousarray(seed, dtype=np.uint16)
+            sp = seed.ctypes.data
+        if threads <= 1:
+            self.lib.oracle_batch(arena.ctypes.data, off.ctypes.data, length.ctypes.data, sp,
+                                  out.ctypes.data, n, int(complement))
+        else:
+            rc = self.lib.oracle_batch_mt(arena.ctypes.data, off.ctypes.data, length.ctypes.data, sp,
+                                          out.ctypes.data, n, int(complement), int(threads))
+            if rc != 0:
+                raise RuntimeError("oracle_batch_mt: thread creation failed")
+        return out
+
+
+    def time_ones_comp(self, data: bytes, iters: int) -> float:
+        """ns per compute_ones_comp(0, data) call (benches/util_bench.rs:20-45 equivalent)."""
+        b = bytes(data)
+        return float(self.lib.oracle_time_ones_comp(b, len(b), iters))
+
+
+_ORACLE: Oracle | None = None
+
+
+def get_oracle() -> Oracle:
+    global _ORACLE
+    if _ORACLE is None:
+        _ORACLE = Oracle()
+    return _ORACLE

@@ -1,0 +1,122 @@
+"""ctypes binding of librns_checksum.so (include/rns_checksum.h).
+
+The product path has no CPU fallback for batches: if the library is missing,
+``load()`` raises ``ChecksumLibraryMissing``; if no gfx950 device is usable the
+batch entry points return RNS_E_NODEVICE and the Python layer raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "librns_checksum.so")
+
+RNS_OK = 0
+RNS_E_INVALID = -1
+RNS_E_EMPTY = -2
+RNS_E_BOUNDS = -3
+RNS_E_NODEVICE = -4
+RNS_E_ORDER = -5
+RNS_E_TOOLARGE = -6
+RNS_E_HIP_BASE = -1000
+RNS_FLAG_COMPLEMENT = 0x1
+
+# Every symbol include/rns_checksum.h declares (tests/test_abi.py checks the header,
+# this list and the library's dynamic symbol table agree).
+EXPORTED_SYMBOLS = (
+    "rns_compute_ones_comp",
+    "rns_compute_checksum",
+    "rns_compute_buffer_ones_comp",
+    "rns_compute_pseudo_header_checksum",
+    "rns_csum_batch_dev",
+    "rns_csum_batch_strided_dev",
+    "rns_csum_batch_dev_cfg",
+    "rns_host_ctx_create",
+    "rns_host_ctx_destroy",
+    "rns_csum_batch_host",
+    "rns_host_alloc",
+    "rns_host_free",
+    "rns_fill_splitmix64_dev",
+    "rns_abi_version",
+    "rns_strerror",
+    "rns_build_info",
+    "rns_device_count",
+)
+
+
+class ChecksumLibraryMissing(RuntimeError):
+    """librns_checksum.so is not built: run __graft_entry__.build() (or `make`)."""
+
+
+class ChecksumError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        self.status = status
+        super().__init__(f"{what}: {strerror(status)} (status {status})")
+
+
+class RnsIovec(ctypes.Structure):
+    """`#[repr(C)] struct IOVec { base: *const u8, len: usize }` (netif.rs:24-29)."""
+    _fields_ = [("base", ctypes.c_void_p), ("len", ctypes.c_size_t)]
+
+
+class RnsIpAddr(ctypes.Structure):
+    """C form of `enum IPAddr { V4([u8;4]), V6([u8;16]) }` (util.rs:22-26)."""
+    _fields_ = [("version", ctypes.c_uint32), ("bytes", ctypes.c_uint8 * 16)]
+
+
+_LIB = None
+_LOCK = threading.Lock()
+
+_vp, _u8, _u16, _u32, _u64, _i32, _int, _sz = (
+    ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64,
+    ctypes.c_int32, ctypes.c_int, ctypes.c_size_t)
+
+_SIGNATURES = {
+    "rns_compute_ones_comp": (_i32, [_u16, _vp, _sz]),
+    "rns_compute_checksum": (_i32, [_vp, _sz]),
+    "rns_compute_buffer_ones_comp": (_i32, [_u16, ctypes.POINTER(RnsIovec), _sz]),
+    "rns_compute_pseudo_header_checksum": (_i32, [ctypes.POINTER(RnsIpAddr), ctypes.POINTER(RnsIpAddr), _u64, _u8]),
+    "rns_csum_batch_dev": (_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp]),
+    "rns_csum_batch_strided_dev": (_int, [_vp, _u64, _u64, _u64, _u32, _vp, _vp, _u32, _u32, _vp, _vp]),
+    "rns_csum_batch_dev_cfg": (_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _vp, _vp]),
+    "rns_host_ctx_create": (_int, [_int, _u64, _u32, ctypes.POINTER(_vp)]),
+    "rns_host_ctx_destroy": (_int, [_vp]),
+    "rns_csum_batch_host": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32]),
+    "rns_host_alloc": (_int, [_u64, ctypes.POINTER(_vp)]),
+    "rns_host_free": (_int, [_vp]),
+    "rns_fill_splitmix64_dev": (_int, [_vp, _u64, _u64, _vp]),
+    "rns_abi_version": (_int, []),
+    "rns_strerror": (ctypes.c_char_p, [_int]),
+    "rns_build_info": (ctypes.c_char_p, []),
+    "rns_device_count": (_int, []),
+}
+
+
+def load() -> ctypes.CDLL:
+    """Load the in-tree library (raises ChecksumLibraryMissing if it was not built)."""
+    global _LIB
+    with _LOCK:
+        if _LIB is None:
+            if not os.path.exists(LIB_PATH):
+                raise ChecksumLibraryMissing(f"{LIB_PATH} not found; run __graft_entry__.build()")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in _SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _LIB = lib
+    return _LIB
+
+
+def strerror(status: int) -> str:
+    try:
+        return load().rns_strerror(status).decode()
+    except ChecksumLibraryMissing:
+        return f"status {status}"
+
+
+def check(status: int, what: str) -> None:
+    if status != RNS_OK:
+        raise ChecksumError(status, what)

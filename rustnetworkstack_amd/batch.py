@@ -1,0 +1,197 @@
+"""Batched checksums on the GPU (device-resident and host-resident), over the C ABI.
+
+The reference has no batch API: every packet's checksum is one
+util::compute_ones_comp call on the thread handling it.  A batch
+here is a packet ARENA (one uint8 buffer) plus per-packet descriptors:
+
+* ``off``  — int64 byte offset of each packet in the arena (any alignment);
+* ``length`` — int32 length in bytes;
+* ``seed`` — optional 16-bit seed per packet (the pseudo-header sum callers
+  pass as in_checksum / initial_sum: tcp.rs:845-848, udp.rs:158-168, icmp.rs:63-71);
+* ``complement`` — store ``0xffff ^ sum`` (what every call site stores or tests).
+
+PyTorch only provides device memory and the stream; the compute is the
+hand-written gfx950 kernel in csrc/rns_checksum.hip.  There is no CPU fallback:
+a missing library or device raises.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _require_cuda(t: torch.Tensor, name: str, dtypes) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name} must be on a GPU device (got {t.device}); there is no CPU fallback")
+    if t.dtype not in dtypes:
+        raise TypeError(f"{name} dtype {t.dtype} not in {dtypes}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+_U16 = (torch.uint16, torch.int16)
+
+
+def _stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def csum_batch(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, seed: torch.Tensor | None = None,
+               *, complement: bool = False, out: torch.Tensor | None = None, len_hint: int = 0,
+               bad: torch.Tensor | None = None, shape: tuple[int, int, int] | None = None) -> torch.Tensor:
+    """Checksum every packet of a device-resident batch; returns uint16 [n] on the same device.
+
+    Launches on the current torch stream of ``arena``'s device and returns
+    without synchronising.  A packet outside the arena yields 0 and increments
+    ``bad`` (int32 [1] device tensor) if given.  ``shape`` = (lanes_per_packet,
+    unroll, max_blocks) overrides the kernel shape (tuning).
+    """
+    _require_cuda(arena, "arena", (torch.uint8,))
+    _require_cuda(off, "off", (torch.int64,))
+    _require_cuda(length, "length", (torch.int32,))
+    n = off.numel()
+    if length.numel() != n:
+        raise ValueError("off and length must have the same number of packets")
+    if n >= 2 ** 32:
+        raise ValueError("at most 2^32-1 packets per call")
+    dev = arena.device
+    for name, t in (("off", off), ("length", length)):
+        if t.device != dev:
+            raise ValueError(f"{name} is on {t.device}, arena on {dev}")
+    seed_ptr = None
+    if seed is not None:
+        _require_cuda(seed, "seed", _U16)
+        if seed.numel() != n or seed.device != dev:
+            raise ValueError("seed must have one entry per packet on the arena's device")
+        seed_ptr = seed.data_ptr()
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint16, device=dev)
+    else:
+        _require_cuda(out, "out", _U16)
+        if out.numel() != n or out.device != dev:
+            raise ValueError("out must have one entry per packet on the arena's device")
+    bad_ptr = None
+    if bad is not None:
+        _require_cuda(bad, "bad", (torch.int32,))
+        bad_ptr = bad.data_ptr()
+    if n == 0:
+        return out
+    lib = _lib.load()
+    flags = _lib.RNS_FLAG_COMPLEMENT if complement else 0
+    with torch.cuda.device(dev):
+        stream = _stream_handle(dev)
+        if shape is None:
+            st = lib.rns_csum_batch_dev(arena.data_ptr(), arena.numel(), off.data_ptr(), length.data_ptr(),
+                                        seed_ptr, out.data_ptr(), n, flags, int(len_hint), bad_ptr, stream)
+        else:
+            g, u, mb = shape
+            st = lib.rns_csum_batch_dev_cfg(arena.data_ptr(), arena.numel(), off.data_ptr(), length.data_ptr(),
+                                            seed_ptr, out.data_ptr(), n, flags, g, u, mb, bad_ptr, stream)
+    _lib.check(st, "rns_csum_batch_dev")
+    return out
+
+
+def csum_batch_strided(arena: torch.Tensor, n: int, stride: int, length: int, *, first_off: int = 0,
+                       seed: torch.Tensor | None = None, complement: bool = False,
+                       out: torch.Tensor | None = None, bad: torch.Tensor | None = None) -> torch.Tensor:
+    """Packets at a fixed stride: packet i = arena[first_off + i*stride : + length]."""
+    _require_cuda(arena, "arena", (torch.uint8,))
+    dev = arena.device
+    seed_ptr = None
+    if seed is not None:
+        _require_cuda(seed, "seed", _U16)
+        if seed.numel() != n:
+            raise ValueError("seed must have one entry per packet")
+        seed_ptr = seed.data_ptr()
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint16, device=dev)
+    bad_ptr = bad.data_ptr() if bad is not None else None
+    lib = _lib.load()
+    with torch.cuda.device(dev):
+        st = lib.rns_csum_batch_strided_dev(arena.data_ptr(), arena.numel(), first_off, stride, length, seed_ptr,
+                                            out.data_ptr(), n, _lib.RNS_FLAG_COMPLEMENT if complement else 0,
+                                            bad_ptr, _stream_handle(dev))
+    _lib.check(st, "rns_csum_batch_strided_dev")
+    return out
+
+
+def fill_splitmix64(buf: torch.Tensor, seed: int) -> torch.Tensor:
+    """Fill a device uint8 buffer with the splitmix64 byte stream (same bytes as
+    oracle.splitmix64_bytes(seed, n))."""
+    _require_cuda(buf, "buf", (torch.uint8,))
+    lib = _lib.load()
+    with torch.cuda.device(buf.device):
+        st = lib.rns_fill_splitmix64_dev(buf.data_ptr(), buf.numel(), seed & 0xFFFFFFFFFFFFFFFF,
+                                         _stream_handle(buf.device))
+    _lib.check(st, "rns_fill_splitmix64_dev")
+    return buf
+
+
+class PinnedBuffer:
+    """Page-locked host memory (rns_host_alloc) viewed as a numpy uint8 array."""
+
+    def __init__(self, nbytes: int):
+        lib = _lib.load()
+        p = ctypes.c_void_p()
+        _lib.check(lib.rns_host_alloc(max(nbytes, 1), ctypes.byref(p)), "rns_host_alloc")
+        self.ptr = p.value
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(nbytes, 1)).from_address(self.ptr))[:nbytes]
+
+    def free(self) -> None:
+        if self.ptr:
+            self.array = None
+            _lib.load().rns_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class HostBatcher:
+    """Host-resident batches: chunked H2D, kernel, D2H of results overlapped on
+    ``nstreams`` streams (rns_csum_batch_host).  Offsets must be ascending."""
+
+    def __init__(self, device: int = 0, chunk_bytes: int = 64 << 20, nstreams: int = 3):
+        lib = _lib.load()
+        ctx = ctypes.c_void_p()
+        _lib.check(lib.rns_host_ctx_create(device, chunk_bytes, nstreams, ctypes.byref(ctx)), "rns_host_ctx_create")
+        self.ctx = ctx.value
+
+    def run(self, arena: np.ndarray, off: np.ndarray, length: np.ndarray, seed: np.ndarray | None = None,
+            complement: bool = False, out: np.ndarray | None = None) -> np.ndarray:
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        n = off.shape[0]
+        if out is None:
+            out = np.empty(n, dtype=np.uint16)
+        sp = None
+        if seed is not None:
+            seed = np.ascontiguousarray(seed, dtype=np.uint16)
+            sp = seed.ctypes.data
+        st = _lib.load().rns_csum_batch_host(self.ctx, arena.ctypes.data, arena.shape[0], off.ctypes.data,
+                                             length.ctypes.data, sp, out.ctypes.data, n,
+                                             _lib.RNS_FLAG_COMPLEMENT if complement else 0)
+        _lib.check(st, "rns_csum_batch_host")
+        return out
+
+    def close(self) -> None:
+        if self.ctx:
+            _lib.load().rns_host_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,537 @@
+// Batched Internet (RFC 1071) checksum for MI355X (gfx950, CDNA4).
+//
+// The reference computes compute_ones_comp (src/stack/util.rs:88-106) once per
+// packet on whichever CPU thread handles it.  Here a batch of
+// packets already resident in HBM is checksummed by one launch:
+//
+//   * a packet is owned by a GROUP of G lanes (G = 4..64, a power of two, so a
+//     64-lane wavefront serves 64/G packets at once); the group streams the
+//     packet as 16-byte aligned chunks, lane l taking chunks l, l+G, ...,
+//     U chunks in flight per lane (global_load_dwordx4, fully coalesced);
+//   * bytes outside [start, start+len) in the first / last chunk are masked
+//     to zero, so packets may start at any byte offset and the odd final
+//     byte is the zero-padded word the reference adds as byte << 8;
+//   * each dword is split by two v_dot4_u32_u8 into the sum of the bytes that
+//     are the HIGH half of a big-endian word and the sum of the LOW halves
+//     (which is which depends on the packet start's parity).  The reference's
+//     u32 accumulator is exactly  seed + 256*high + low  (mod 2^32), so the
+//     per-lane u32 partials are summed with wrap-around across the group
+//     (shuffle butterfly) and folded end-around exactly like util.rs:101-103:
+//     bit-exact for every length, including the reference's wrap past 128 KiB;
+//   * one lane per group stores the u16 result (optionally ^ 0xffff).
+//
+// This is a bandwidth-bound integer reduction (~1 byte of HBM per 0.5 VALU
+// op): no MFMA, no LDS staging needed for the data itself.  Roofline: HBM read
+// bandwidth; algorithmic bytes per packet = len + 2.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "rns_checksum.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+struct CsumArgs {
+    const uint8_t *arena;      // 16-byte aligned base
+    uint64_t arena_bytes;      // valid bytes from `arena` (after base_adjust)
+    uint64_t base_adjust;      // added to every packet offset (caller base was not 16-aligned)
+    const uint64_t *off;       // per-packet byte offsets (null in strided mode)
+    const uint32_t *len;       // per-packet lengths (null in strided mode)
+    const uint16_t *seed;      // per-packet seeds, null => 0
+    uint16_t *out;
+    uint32_t *bad;             // optional counter of rejected descriptors
+    uint64_t first_off;        // strided mode
+    uint64_t stride;
+    uint32_t fixed_len;
+    uint32_t n;
+    uint32_t flags;
+};
+
+// Keep bytes [lo, hi) of the 4-byte dword at byte j4 = 4*j of a 16-byte chunk.
+__device__ __forceinline__ uint32_t keep_bytes(uint32_t d, int lo, int hi, int j4)
+{
+    const int a = min(max(lo - j4, 0), 4);
+    const int b = min(max(hi - j4, 0), 4);
+    const uint32_t hm = static_cast<uint32_t>((1ull << (8 * b)) - 1);
+    const uint32_t lm = static_cast<uint32_t>((1ull << (8 * a)) - 1);
+    return d & hm & ~lm;  // b <= a gives 0
+}
+
+template <int G>
+__device__ __forceinline__ uint32_t group_sum(uint32_t v)
+{
+#pragma unroll
+    for (int m = G / 2; m >= 1; m >>= 1)
+        v += static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), m, 64));
+    return v;
+}
+
+template <int G, int U, bool STRIDED>
+__global__ __launch_bounds__(kBlock) void csum_batch_kernel(const CsumArgs a)
+{
+    static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two in [4,64]");
+    constexpr uint32_t kGroups = kBlock / G;
+    const uint32_t lane = threadIdx.x & (G - 1);
+    const uint32_t grp_stride = gridDim.x * kGroups;
+
+    for (uint32_t p = blockIdx.x * kGroups + threadIdx.x / G; p < a.n; p += grp_stride) {
+        uint64_t start;
+        uint32_t L;
+        if constexpr (STRIDED) {
+            start = a.first_off + static_cast<uint64_t>(p) * a.stride;
+            L = a.fixed_len;
+        } else {
+            start = a.off[p];
+            L = a.len[p];
+        }
+        start += a.base_adjust;
+        const bool ok = start <= a.arena_bytes && L <= a.arena_bytes - start;
+
+        uint32_t hi_sum = 0, lo_sum = 0;
+        if (ok && L != 0) {
+            const uint32_t s = static_cast<uint32_t>(start & 15);
+            const uint8_t *base = a.arena + (start - s);
+            const uint64_t span = s + static_cast<uint64_t>(L);
+            const uint32_t nch = static_cast<uint32_t>((span + 15) >> 4);
+            const uint32_t last = nch - 1;
+            const int e = static_cast<int>(span - (static_cast<uint64_t>(last) << 4));  // 1..16
+            // Bytes at even offsets from the packet start are BE high halves.
+            const uint32_t w_hi = (start & 1) ? 0x01000100u : 0x00010001u;
+            const uint32_t w_lo = w_hi ^ 0x01010101u;
+
+            for (uint32_t c0 = lane; c0 < nch; c0 += G * U) {
+                uint4 v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t c = c0 + u * G;
+                    if (c < nch)
+                        v[u] = *reinterpret_cast<const uint4 *>(base + (static_cast<uint64_t>(c) << 4));
+                    else
+                        v[u] = make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t c = c0 + u * G;
+                    if (c == 0 || c == last) {
+                        const int lo = (c == 0) ? static_cast<int>(s) : 0;
+                        const int hi = (c == last) ? e : 16;
+                        v[u].x = keep_bytes(v[u].x, lo, hi, 0);
+                        v[u].y = keep_bytes(v[u].y, lo, hi, 4);
+                        v[u].z = keep_bytes(v[u].z, lo, hi, 8);
+                        v[u].w = keep_bytes(v[u].w, lo, hi, 12);
+                    }
+                    hi_sum = __builtin_amdgcn_udot4(v[u].x, w_hi, hi_sum, false);
+                    lo_sum = __builtin_amdgcn_udot4(v[u].x, w_lo, lo_sum, false);
+                    hi_sum = __builtin_amdgcn_udot4(v[u].y, w_hi, hi_sum, false);
+                    lo_sum = __builtin_amdgcn_udot4(v[u].y, w_lo, lo_sum, false);
+                    hi_sum = __builtin_amdgcn_udot4(v[u].z, w_hi, hi_sum, false);
+                    lo_sum = __builtin_amdgcn_udot4(v[u].z, w_lo, lo_sum, false);
+                    hi_sum = __builtin_amdgcn_udot4(v[u].w, w_hi, hi_sum, false);
+                    lo_sum = __builtin_amdgcn_udot4(v[u].w, w_lo, lo_sum, false);
+                }
+            }
+        }
+        // sum of BE words of this lane's bytes, mod 2^32 (the reference's u32 wraps the same way)
+        const uint32_t words = group_sum<G>((hi_sum << 8) + lo_sum);
+
+        if (lane == 0) {
+            const uint32_t sd = a.seed ? a.seed[p] : 0u;
+            uint32_t acc = sd + words;  // util.rs:89-99 (mod 2^32)
+            while (acc > 0xffff)        // util.rs:101-103
+                acc = (acc & 0xffff) + (acc >> 16);
+            if (a.flags & RNS_FLAG_COMPLEMENT)
+                acc ^= 0xffff;
+            if (!ok) {
+                acc = 0;
+                if (a.bad)
+                    atomicAdd(a.bad, 1u);
+            }
+            a.out[p] = static_cast<uint16_t>(acc);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void splitmix64_fill_kernel(uint8_t *buf, uint64_t nbytes, uint64_t seed)
+{
+    const uint64_t nwords = (nbytes + 7) / 8;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nwords; i += stride) {
+        uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z = z ^ (z >> 31);
+        if ((i + 1) * 8 <= nbytes) {
+            reinterpret_cast<uint64_t *>(buf)[i] = z;
+        } else {
+            for (uint64_t b = i * 8; b < nbytes; ++b)
+                buf[b] = static_cast<uint8_t>(z >> (8 * (b - i * 8)));
+        }
+    }
+}
+
+inline int hip_status(hipError_t e) { return e == hipSuccess ? RNS_OK : RNS_E_HIP_BASE - static_cast<int>(e); }
+
+template <int G, int U, bool S>
+int launch_shape(const CsumArgs &a, uint32_t max_blocks, hipStream_t st)
+{
+    constexpr uint32_t kGroups = kBlock / G;
+    uint64_t blocks = (static_cast<uint64_t>(a.n) + kGroups - 1) / kGroups;
+    if (max_blocks != 0 && blocks > max_blocks)
+        blocks = max_blocks;
+    if (blocks == 0)
+        return RNS_OK;
+    hipLaunchKernelGGL((csum_batch_kernel<G, U, S>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, st, a);
+    return hip_status(hipGetLastError());
+}
+
+template <bool S>
+int dispatch(const CsumArgs &a, uint32_t G, uint32_t U, uint32_t max_blocks, hipStream_t st)
+{
+#define RNS_SHAPE(g, u) \
+    if (G == g && U == u) return launch_shape<g, u, S>(a, max_blocks, st);
+    RNS_SHAPE(4, 1) RNS_SHAPE(4, 2) RNS_SHAPE(4, 4)
+    RNS_SHAPE(8, 1) RNS_SHAPE(8, 2) RNS_SHAPE(8, 4)
+    RNS_SHAPE(16, 1) RNS_SHAPE(16, 2) RNS_SHAPE(16, 4)
+    RNS_SHAPE(32, 1) RNS_SHAPE(32, 2) RNS_SHAPE(32, 4)
+    RNS_SHAPE(64, 1) RNS_SHAPE(64, 2) RNS_SHAPE(64, 4)
+#undef RNS_SHAPE
+    return RNS_E_INVALID;
+}
+
+// Lanes per packet and chunks in flight per lane for a typical packet length.
+void pick_shape(uint32_t len_hint, uint32_t *G, uint32_t *U)
+{
+    const uint32_t chunks = len_hint ? (len_hint + 15) / 16 + 1 : 96;
+    uint32_t g = 4;
+    while (g < 64 && g * 2 < chunks)
+        g *= 2;
+    *G = g;
+    *U = (chunks > 2 * g) ? 4 : 2;
+}
+
+int check_device()
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        return RNS_E_NODEVICE;
+    }
+    return RNS_OK;
+}
+
+// Fill CsumArgs for a caller arena base that may not be 16-byte aligned.
+void set_arena(CsumArgs &a, const uint8_t *arena, uint64_t arena_bytes)
+{
+    const uintptr_t p = reinterpret_cast<uintptr_t>(arena);
+    a.base_adjust = p & 15;
+    a.arena = reinterpret_cast<const uint8_t *>(p - a.base_adjust);
+    a.arena_bytes = arena_bytes + a.base_adjust;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// host-resident pipeline context
+// ---------------------------------------------------------------------------
+struct rns_host_ctx {
+    struct Slot {
+        hipStream_t stream = nullptr;
+        hipEvent_t done = nullptr;
+        uint8_t *d_arena = nullptr;
+        uint64_t *d_off = nullptr;
+        uint32_t *d_len = nullptr;
+        uint16_t *d_seed = nullptr;
+        uint16_t *d_out = nullptr;
+        uint64_t *h_off = nullptr;  // pinned descriptor staging
+        uint32_t *h_len = nullptr;
+        uint16_t *h_seed = nullptr;
+        uint16_t *h_out = nullptr;
+        bool busy = false;
+        uint32_t i0 = 0, cnt = 0;
+    };
+    int device = 0;
+    uint64_t chunk_bytes = 0;
+    uint32_t chunk_packets = 0;
+    std::vector<Slot> slots;
+    std::mutex mu;
+};
+
+namespace {
+
+void free_ctx(rns_host_ctx *c)
+{
+    if (!c)
+        return;
+    (void)hipSetDevice(c->device);
+    for (auto &s : c->slots) {
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+        if (s.done) (void)hipEventDestroy(s.done);
+        if (s.stream) (void)hipStreamDestroy(s.stream);
+        (void)hipFree(s.d_arena); (void)hipFree(s.d_off); (void)hipFree(s.d_len);
+        (void)hipFree(s.d_seed); (void)hipFree(s.d_out);
+        (void)hipHostFree(s.h_off); (void)hipHostFree(s.h_len);
+        (void)hipHostFree(s.h_seed); (void)hipHostFree(s.h_out);
+    }
+    delete c;
+}
+
+int drain_slot(rns_host_ctx::Slot &s, uint16_t *h_out)
+{
+    if (!s.busy)
+        return RNS_OK;
+    s.busy = false;
+    int st = hip_status(hipEventSynchronize(s.done));
+    if (st == RNS_OK)
+        std::memcpy(h_out + s.i0, s.h_out, static_cast<size_t>(s.cnt) * sizeof(uint16_t));
+    return st;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rns_csum_batch_dev_cfg(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off,
+                           const uint32_t *d_len, const uint16_t *d_seed, uint16_t *d_out, uint32_t n,
+                           uint32_t flags, uint32_t lanes_per_packet, uint32_t unroll,
+                           uint32_t max_blocks, uint32_t *d_bad, void *stream)
+{
+    if (n == 0)
+        return RNS_OK;
+    if (!d_arena || !d_off || !d_len || !d_out)
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    CsumArgs a{};
+    set_arena(a, d_arena, arena_bytes);
+    a.off = d_off;
+    a.len = d_len;
+    a.seed = d_seed;
+    a.out = d_out;
+    a.bad = d_bad;
+    a.n = n;
+    a.flags = flags;
+    return dispatch<false>(a, lanes_per_packet, unroll, max_blocks, static_cast<hipStream_t>(stream));
+}
+
+int rns_csum_batch_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off,
+                       const uint32_t *d_len, const uint16_t *d_seed, uint16_t *d_out, uint32_t n,
+                       uint32_t flags, uint32_t len_hint, uint32_t *d_bad, void *stream)
+{
+    uint32_t G, U;
+    pick_shape(len_hint, &G, &U);
+    return rns_csum_batch_dev_cfg(d_arena, arena_bytes, d_off, d_len, d_seed, d_out, n, flags, G, U, 0,
+                                  d_bad, stream);
+}
+
+int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uint64_t first_off,
+                               uint64_t stride, uint32_t len, const uint16_t *d_seed, uint16_t *d_out,
+                               uint32_t n, uint32_t flags, uint32_t *d_bad, void *stream)
+{
+    if (n == 0)
+        return RNS_OK;
+    if (!d_arena || !d_out)
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    CsumArgs a{};
+    set_arena(a, d_arena, arena_bytes);
+    a.seed = d_seed;
+    a.out = d_out;
+    a.bad = d_bad;
+    a.first_off = first_off;
+    a.stride = stride;
+    a.fixed_len = len;
+    a.n = n;
+    a.flags = flags;
+    uint32_t G, U;
+    pick_shape(len, &G, &U);
+    return dispatch<true>(a, G, U, 0, static_cast<hipStream_t>(stream));
+}
+
+int rns_host_ctx_create(int device, uint64_t chunk_bytes, uint32_t nstreams, rns_host_ctx **out)
+{
+    if (!out || nstreams == 0 || nstreams > 16 || chunk_bytes < 4096)
+        return RNS_E_INVALID;
+    *out = nullptr;
+    if (int st = check_device())
+        return st;
+    int st = hip_status(hipSetDevice(device));
+    if (st)
+        return st;
+    rns_host_ctx *c = new (std::nothrow) rns_host_ctx;
+    if (!c)
+        return RNS_E_INVALID;
+    c->device = device;
+    c->chunk_bytes = (chunk_bytes + 255) & ~255ull;
+    c->chunk_packets = static_cast<uint32_t>(std::min<uint64_t>(c->chunk_bytes / 16, 1u << 24));
+    c->slots.resize(nstreams);
+    const size_t np = c->chunk_packets;
+    for (auto &s : c->slots) {
+        hipError_t e = hipSuccess;
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&s.d_arena), c->chunk_bytes + 256);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&s.d_off), np * sizeof(uint64_t));
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&s.d_len), np * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&s.d_seed), np * sizeof(uint16_t));
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&s.d_out), np * sizeof(uint16_t));
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&s.h_off), np * sizeof(uint64_t), 0);
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&s.h_len), np * sizeof(uint32_t), 0);
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&s.h_seed), np * sizeof(uint16_t), 0);
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&s.h_out), np * sizeof(uint16_t), 0);
+        if (e != hipSuccess) {
+            free_ctx(c);
+            return hip_status(e);
+        }
+    }
+    *out = c;
+    return RNS_OK;
+}
+
+int rns_host_ctx_destroy(rns_host_ctx *ctx)
+{
+    free_ctx(ctx);
+    return RNS_OK;
+}
+
+int rns_csum_batch_host(rns_host_ctx *ctx, const uint8_t *h_arena, uint64_t arena_bytes,
+                        const uint64_t *h_off, const uint32_t *h_len, const uint16_t *h_seed,
+                        uint16_t *h_out, uint32_t n, uint32_t flags)
+{
+    if (!ctx)
+        return RNS_E_INVALID;
+    if (n == 0)
+        return RNS_OK;
+    if (!h_arena || !h_off || !h_len || !h_out)
+        return RNS_E_INVALID;
+    // Validate the whole batch first so a bad descriptor never reaches the device.
+    for (uint32_t i = 0; i < n; ++i) {
+        if (h_off[i] > arena_bytes || h_len[i] > arena_bytes - h_off[i])
+            return RNS_E_BOUNDS;
+        if (i && h_off[i] < h_off[i - 1])
+            return RNS_E_ORDER;
+    }
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    int st = hip_status(hipSetDevice(ctx->device));
+    if (st)
+        return st;
+    const size_t nslots = ctx->slots.size();
+    size_t k = 0;
+    uint32_t i0 = 0;
+    while (i0 < n && st == RNS_OK) {
+        // Chunk: packets [i0, i1) whose bytes fit one staging buffer.
+        const uint64_t lo = h_off[i0] & ~255ull;  // keeps 16-byte alignment and byte parity
+        uint64_t hi = lo;
+        uint32_t i1 = i0;
+        while (i1 < n && i1 - i0 < ctx->chunk_packets) {
+            const uint64_t end = std::max(hi, h_off[i1] + h_len[i1]);
+            if (end - lo > ctx->chunk_bytes)
+                break;
+            hi = end;
+            ++i1;
+        }
+        if (i1 == i0)
+            return RNS_E_TOOLARGE;
+        auto &s = ctx->slots[k++ % nslots];
+        st = drain_slot(s, h_out);
+        if (st)
+            break;
+        const uint32_t cnt = i1 - i0;
+        std::memcpy(s.h_off, h_off + i0, cnt * sizeof(uint64_t));
+        std::memcpy(s.h_len, h_len + i0, cnt * sizeof(uint32_t));
+        if (h_seed)
+            std::memcpy(s.h_seed, h_seed + i0, cnt * sizeof(uint16_t));
+        hipError_t e = hipMemcpyAsync(s.d_arena, h_arena + lo, hi - lo, hipMemcpyHostToDevice, s.stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(s.d_off, s.h_off, cnt * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(s.d_len, s.h_len, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream);
+        if (e == hipSuccess && h_seed)
+            e = hipMemcpyAsync(s.d_seed, s.h_seed, cnt * sizeof(uint16_t), hipMemcpyHostToDevice, s.stream);
+        if (e != hipSuccess) {
+            st = hip_status(e);
+            break;
+        }
+        // Offsets stay absolute: the kernel sees arena = staging - lo (never dereferenced below staging).
+        CsumArgs a{};
+        a.arena = s.d_arena - lo;
+        a.arena_bytes = hi;
+        a.base_adjust = 0;
+        a.off = s.d_off;
+        a.len = s.d_len;
+        a.seed = h_seed ? s.d_seed : nullptr;
+        a.out = s.d_out;
+        a.n = cnt;
+        a.flags = flags;
+        uint32_t G, U;
+        pick_shape(static_cast<uint32_t>(std::min<uint64_t>((hi - lo) / cnt, 1u << 30)), &G, &U);
+        st = dispatch<false>(a, G, U, 0, s.stream);
+        if (st)
+            break;
+        e = hipMemcpyAsync(s.h_out, s.d_out, cnt * sizeof(uint16_t), hipMemcpyDeviceToHost, s.stream);
+        if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
+        if (e != hipSuccess) {
+            st = hip_status(e);
+            break;
+        }
+        s.busy = true;
+        s.i0 = i0;
+        s.cnt = cnt;
+        i0 = i1;
+    }
+    for (auto &s : ctx->slots) {
+        int d = drain_slot(s, h_out);
+        if (st == RNS_OK)
+            st = d;
+    }
+    return st;
+}
+
+int rns_host_alloc(uint64_t bytes, void **out)
+{
+    if (!out)
+        return RNS_E_INVALID;
+    *out = nullptr;
+    if (int st = check_device())
+        return st;
+    return hip_status(hipHostMalloc(out, bytes, 0));
+}
+
+int rns_host_free(void *p) { return hip_status(hipHostFree(p)); }
+
+int rns_fill_splitmix64_dev(uint8_t *d_buf, uint64_t nbytes, uint64_t seed, void *stream)
+{
+    if (nbytes == 0)
+        return RNS_OK;
+    if (!d_buf || (reinterpret_cast<uintptr_t>(d_buf) & 7))
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    const uint64_t words = (nbytes + 7) / 8;
+    const uint32_t blocks = static_cast<uint32_t>(std::min<uint64_t>((words + kBlock - 1) / kBlock, 8192));
+    hipLaunchKernelGGL(splitmix64_fill_kernel, dim3(blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                       d_buf, nbytes, seed);
+    return hip_status(hipGetLastError());
+}
+
+const char *rns_build_info(void)
+{
+    return "rns_checksum abi=1 offload-arch=gfx950 kernel=csum_batch_kernel<G,U> (dot4 BE-half sums, wave64)";
+}
+
+int rns_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+}  // extern "C"

@@ -1,0 +1,136 @@
+"""Synthetic packet batches for the configurations BASELINE.json names.
+
+SURVEY §8d: packet bytes from splitmix64 (seed 0x5EED_C0DE), per-packet 16-bit
+seeds from the same generator family, packet starts 16-byte aligned in the
+arena (padding bytes are not counted as payload).
+
+========  =====================  ============================================
+name      packets                BASELINE.json config
+========  =====================  ============================================
+c1_512B   1 x 512 B (host)       cargo bench util_bench (CPU, single buffer)
+c2_64B    2^20 x 64 B            1 GPU minimum-size packets
+c3_1500B  2^20 x 1500 B          1 GPU MTU packets — the headline metric
+c4_9000B  2^18 x 9000 B          1 GPU jumbo frames
+c5_imix   2^23 IMIX 40/576/1500  8 GPU mixed sizes, sharded by packet index
+          in a 7:4:1 ratio
+========  =====================  ============================================
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+DATA_SEED = 0x5EEDC0DE
+SEED_STREAM = 0x5EED5EED  # xor-ed into DATA_SEED for the per-packet seed stream
+ALIGN = 16
+
+CONFIGS = {
+    "c2_64B": dict(n=1 << 20, kind="fixed", length=64),
+    "c3_1500B": dict(n=1 << 20, kind="fixed", length=1500),
+    "c4_9000B": dict(n=1 << 18, kind="fixed", length=9000),
+    "c5_imix": dict(n=1 << 23, kind="imix"),
+}
+HEADLINE = "c3_1500B"
+IMIX_SIZES = (40, 576, 1500)  # 7:4:1
+
+
+def splitmix64(seed: int, count: int, start: int = 0) -> np.ndarray:
+    """z_i = mix(seed + (start+i+1) * 0x9E3779B97F4A7C15) — the stream
+    rns_fill_splitmix64_dev writes on the device."""
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed & 0xFFFFFFFFFFFFFFFF) + np.arange(start + 1, start + count + 1, dtype=np.uint64) * np.uint64(
+            0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+@dataclass
+class Layout:
+    """Host-side description of a batch: where each packet sits in the arena."""
+    name: str
+    off: np.ndarray      # uint64
+    length: np.ndarray   # uint32
+    seed: np.ndarray     # uint16
+    arena_bytes: int
+    data_seed: int
+
+    @property
+    def n(self) -> int:
+        return int(self.off.shape[0])
+
+    @property
+    def payload_bytes(self) -> int:
+        return int(self.length.astype(np.uint64).sum())
+
+    @property
+    def mean_len(self) -> float:
+        return self.payload_bytes / max(self.n, 1)
+
+
+def imix_lengths(n: int, seed: int) -> np.ndarray:
+    r = splitmix64(seed ^ 0x1A1A1A1A, n) % np.uint64(12)
+    out = np.full(n, IMIX_SIZES[2], dtype=np.uint32)
+    out[r < 11] = IMIX_SIZES[1]
+    out[r < 7] = IMIX_SIZES[0]
+    return out
+
+
+def make_layout(name: str, n: int | None = None, data_seed: int = DATA_SEED, shard: tuple[int, int] = (0, 1),
+                align: int = ALIGN) -> Layout:
+    """Packets of config `name`; `shard=(rank, world)` keeps the contiguous
+    packet-index range ceil(n/world) of that rank."""
+    cfg = CONFIGS[name]
+    total = cfg["n"] if n is None else n
+    if cfg["kind"] == "fixed":
+        length_all = None
+    else:
+        length_all = imix_lengths(total, data_seed)
+    rank, world = shard
+    per = -(-total // world)
+    lo, hi = min(rank * per, total), min((rank + 1) * per, total)
+    count = hi - lo
+    if length_all is None:
+        length = np.full(count, cfg["length"], dtype=np.uint32)
+    else:
+        length = length_all[lo:hi].copy()
+    padded = (length.astype(np.uint64) + np.uint64(align - 1)) & ~np.uint64(align - 1)
+    off = np.zeros(count, dtype=np.uint64)
+    if count > 1:
+        np.cumsum(padded[:-1], out=off[1:])
+    arena_bytes = int(off[-1] + padded[-1]) if count else 0
+    seed = (splitmix64(data_seed ^ SEED_STREAM, count, start=lo) & np.uint64(0xFFFF)).astype(np.uint16)
+    return Layout(name=name, off=off, length=length, seed=seed, arena_bytes=arena_bytes,
+                  data_seed=(data_seed + rank) & 0xFFFFFFFFFFFFFFFF)
+
+
+class DeviceBatch:
+    """A Layout materialised in HBM: arena filled with splitmix64 bytes on the
+    device, descriptors uploaded once (inputs resident before any timing)."""
+
+    def __init__(self, layout: Layout, device):
+        import torch
+
+        from .batch import fill_splitmix64
+
+        self.layout = layout
+        self.device = torch.device(device)
+        # +16 slack keeps the arena a whole number of 16-byte chunks
+        self.arena = torch.empty(layout.arena_bytes + 16, dtype=torch.uint8, device=self.device)
+        fill_splitmix64(self.arena, layout.data_seed)
+        self.off = torch.from_numpy(layout.off.view(np.int64)).to(self.device)
+        self.length = torch.from_numpy(layout.length.view(np.int32)).to(self.device)
+        self.seed = torch.from_numpy(layout.seed.view(np.int16)).to(self.device)
+        self.out = torch.empty(layout.n, dtype=torch.uint16, device=self.device)
+
+    def run(self, complement: bool = False, shape=None):
+        from .batch import csum_batch
+        return csum_batch(self.arena, self.off, self.length, self.seed, complement=complement, out=self.out,
+                          len_hint=int(round(self.layout.mean_len)), shape=shape)
+
+    def host_arena(self) -> np.ndarray:
+        return self.arena.cpu().numpy()
+
+    def host_out(self) -> np.ndarray:
+        return self.out.view(__import__("torch").int16).cpu().numpy().view(np.uint16)

@@ -1,0 +1,213 @@
+"""Parity of the gfx950 HIP path with the oracle (bit-exact), through the C ABI.
+
+Small cases compare every packet with the committed golden fixtures and with
+the C oracle; full BASELINE.json sizes compare every packet with the C oracle
+(multi-threaded) and check size-independent properties (transmit-fill then
+receive-verify gives 0 for every packet).  Runs on one MI355X: one process,
+no repeated launches of the runner.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import sweep_arena
+from oracle import oracle as O
+from rustnetworkstack_amd import _lib
+from rustnetworkstack_amd.batch import HostBatcher, PinnedBuffer, csum_batch, csum_batch_strided, fill_splitmix64
+from rustnetworkstack_amd.workloads import DeviceBatch, make_layout
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+SHAPES = [(g, u) for g in (4, 8, 16, 32, 64) for u in (1, 2, 4)]
+
+
+def host_u16(t: torch.Tensor) -> np.ndarray:
+    torch.cuda.synchronize()
+    return t.view(torch.int16).cpu().numpy().view(np.uint16)
+
+
+def to_dev(a: np.ndarray, dtype_view) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a).view(dtype_view)).to(DEV)
+
+
+def dev_desc(off, ln, sd):
+    return to_dev(off.astype(np.uint64), np.int64), to_dev(ln.astype(np.uint32), np.int32), (
+        None if sd is None else to_dev(sd.astype(np.uint16), np.int16))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu_present():
+    if not torch.cuda.is_available() or _lib.load().rns_device_count() == 0:
+        pytest.fail("gpu tests need a GPU (the HIP path has no CPU fallback)")
+
+
+def test_device_splitmix_fill_matches_oracle():
+    for nbytes in (1, 7, 8, 1 << 20, (1 << 20) + 5):
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+        fill_splitmix64(buf, 0x5EEDC0DE)
+        torch.cuda.synchronize()
+        assert np.array_equal(buf.cpu().numpy(), O.splitmix64_bytes(0x5EEDC0DE, nbytes))
+
+
+@pytest.fixture(scope="module")
+def sweep_dev(sweep):
+    arena = torch.from_numpy(sweep_arena(sweep)).to(DEV)
+    off, ln, sd = dev_desc(np.array(sweep["offset"]), np.array(sweep["length"]), np.array(sweep["pkt_seed"]))
+    return arena, off, ln, sd, np.array(sweep["expect"], dtype=np.uint16)
+
+
+@pytest.mark.parametrize("g,u", SHAPES)
+@pytest.mark.parametrize("max_blocks", [0, 37])
+def test_golden_sweep_every_shape(sweep_dev, g, u, max_blocks):
+    arena, off, ln, sd, expect = sweep_dev
+    out = csum_batch(arena, off, ln, sd, shape=(g, u, max_blocks))
+    assert np.array_equal(host_u16(out), expect)
+    outc = csum_batch(arena, off, ln, sd, complement=True, shape=(g, u, max_blocks))
+    assert np.array_equal(host_u16(outc), expect ^ 0xFFFF)
+
+
+def test_golden_sweep_default_shapes(sweep_dev):
+    arena, off, ln, sd, expect = sweep_dev
+    for hint in (0, 40, 64, 576, 1500, 9000, 65535):
+        assert np.array_equal(host_u16(csum_batch(arena, off, ln, sd, len_hint=hint)), expect)
+
+
+def test_length_by_alignment_sweep(oracle):
+    """Every length 1..2048 at every start offset mod 16, random seeds, vs the C oracle."""
+    arena_np = O.splitmix64_bytes(0xA11A, 4 << 20)
+    lens = np.repeat(np.arange(1, 2049, dtype=np.uint32), 16)
+    align = np.tile(np.arange(16, dtype=np.uint64), 2048)
+    base = (O.splitmix64_words(0xB0B, lens.size) % np.uint64((4 << 20) - 4096)) & ~np.uint64(15)
+    off = base + align
+    sd = (O.splitmix64_words(0xC0C, lens.size) & np.uint64(0xFFFF)).astype(np.uint16)
+    expect = oracle.batch(arena_np, off, lens, sd, complement=True)
+    arena = torch.from_numpy(arena_np).to(DEV)
+    d_off, d_len, d_sd = dev_desc(off, lens, sd)
+    for shape in (None, (4, 1, 0), (16, 2, 0), (64, 4, 0), (64, 2, 512)):
+        out = csum_batch(arena, d_off, d_len, d_sd, complement=True, shape=shape, len_hint=1024)
+        assert np.array_equal(host_u16(out), expect), shape
+
+
+def test_edge_patterns_and_zero_handling(oracle):
+    zeros = np.zeros(200016, dtype=np.uint8)
+    ones = np.full(200016, 0xFF, dtype=np.uint8)
+    arena_np = np.concatenate([zeros, ones])
+    rows = []
+    for base in (0, 200016):
+        for L in (1, 2, 3, 64, 1500, 9000, 65535, 131072, 131073, 200001):
+            for a in (0, 1, 5):
+                for s in (0, 1, 0xFFFE, 0xFFFF):
+                    if a + L <= 200016:
+                        rows.append((base + a, L, s))
+    off = np.array([r[0] for r in rows], dtype=np.uint64)
+    ln = np.array([r[1] for r in rows], dtype=np.uint32)
+    sd = np.array([r[2] for r in rows], dtype=np.uint16)
+    expect = oracle.batch(arena_np, off, ln, sd)
+    arena = torch.from_numpy(arena_np).to(DEV)
+    d = dev_desc(off, ln, sd)
+    for shape in (None, (4, 4, 0), (64, 1, 0)):
+        assert np.array_equal(host_u16(csum_batch(arena, *d, shape=shape)), expect), shape
+    # all-zero payload with seed 0 is 0 (checksum 0xffff); all-0xff folds to 0xffff (checksum 0)
+    assert expect[0] == 0 and expect[-1] == 0xFFFF
+
+
+def test_bounds_and_empty_packets():
+    arena = torch.zeros(4096, dtype=torch.uint8, device=DEV)
+    fill_splitmix64(arena, 3)
+    off = np.array([0, 4000, 4096, 4097, 10, 5000, 3], dtype=np.uint64)
+    ln = np.array([16, 96, 0, 0, 0, 1, 4093], dtype=np.uint32)
+    sd = np.array([1, 2, 3, 4, 0xABCD, 6, 7], dtype=np.uint16)
+    bad = torch.zeros(1, dtype=torch.int32, device=DEV)
+    out = host_u16(csum_batch(arena, *dev_desc(off, ln, sd), bad=bad))
+    a = arena.cpu().numpy().tobytes()
+    assert out[0] == O.ones_comp_py(1, a[0:16])
+    assert out[1] == 0                     # 4000+96 > 4096: rejected
+    assert out[2] == 3                     # len 0 at the end: seed (reference panics; API-defined)
+    assert out[3] == 0                     # offset past the end: rejected
+    assert out[4] == 0xABCD                # len 0: seed unchanged
+    assert out[5] == 0                     # rejected
+    assert out[6] == O.ones_comp_py(7, a[3:4096])
+    assert int(bad.item()) == 3
+
+
+def test_unaligned_arena_base(oracle):
+    big = torch.empty(1 << 20, dtype=torch.uint8, device=DEV)
+    fill_splitmix64(big, 99)
+    host = big.cpu().numpy()
+    for shift in (1, 3, 8, 15):
+        view = big[shift:]
+        n = 2000
+        ln = (O.splitmix64_words(shift, n) % np.uint64(1600) + np.uint64(1)).astype(np.uint32)
+        off = (O.splitmix64_words(shift + 100, n) % np.uint64((1 << 20) - 2000)).astype(np.uint64)
+        expect = oracle.batch(host[shift:], off, ln, None, complement=True)
+        out = csum_batch(view, *dev_desc(off, ln, None), complement=True)
+        assert np.array_equal(host_u16(out), expect), shift
+
+
+def test_strided_api(oracle):
+    for L, stride, first in ((64, 64, 0), (1500, 1504, 0), (1500, 1501, 3), (9000, 9008, 16), (40, 48, 7)):
+        n = 5000
+        arena = torch.empty(first + stride * n + 64, dtype=torch.uint8, device=DEV)
+        fill_splitmix64(arena, L)
+        sd_np = (O.splitmix64_words(L, n) & np.uint64(0xFFFF)).astype(np.uint16)
+        sd = to_dev(sd_np, np.int16)
+        out = csum_batch_strided(arena, n, stride, L, first_off=first, seed=sd, complement=True)
+        off = first + np.arange(n, dtype=np.uint64) * np.uint64(stride)
+        expect = oracle.batch(arena.cpu().numpy(), off, np.full(n, L, dtype=np.uint32), sd_np, complement=True)
+        assert np.array_equal(host_u16(out), expect), (L, stride, first)
+
+
+@pytest.mark.parametrize("name", ["c2_64B", "c3_1500B", "c4_9000B", "c5_imix"])
+def test_full_size_configs_bit_exact(oracle, name):
+    """Every packet of every BASELINE.json GPU config, bit-exact against the C oracle."""
+    lay = make_layout(name)
+    b = DeviceBatch(lay, DEV)
+    b.run(complement=False)
+    got = b.host_out()
+    arena = b.host_arena()
+    expect = oracle.batch(arena, lay.off, lay.length, lay.seed, threads=16)
+    assert np.array_equal(got, expect)
+    del b
+    torch.cuda.empty_cache()
+
+
+def test_full_size_transmit_fill_then_receive_verify():
+    """Size-independent property at the headline size: store each packet's complemented
+    checksum into its TCP checksum field (tcp.rs:970-973, field zeroed first as
+    alloc_header does, buf.rs:286-288), then the receive check (tcp.rs:848) gives 0 for all."""
+    lay = make_layout("c3_1500B")
+    b = DeviceBatch(lay, DEV)
+    arena, off = b.arena, b.off
+    field = off.view(-1, 1) + torch.tensor([16, 17], device=DEV)   # header[16..18]
+    arena[field.flatten()] = 0
+    tx = csum_batch(arena, off, b.length, b.seed, complement=True)
+    tx32 = tx.view(torch.int16).to(torch.int32) & 0xFFFF
+    arena[field[:, 0]] = (tx32 >> 8).to(torch.uint8)
+    arena[field[:, 1]] = (tx32 & 0xFF).to(torch.uint8)
+    rx = csum_batch(arena, off, b.length, b.seed, complement=True)
+    assert int((rx.view(torch.int16) != 0).sum().item()) == 0
+    del b
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_host_resident_pipeline(oracle, pinned):
+    lay = make_layout("c5_imix", n=300000)
+    nbytes = lay.arena_bytes
+    if pinned:
+        pb = PinnedBuffer(nbytes)
+        arena = pb.array
+        arena[:] = O.splitmix64_bytes(lay.data_seed, nbytes)
+    else:
+        arena = O.splitmix64_bytes(lay.data_seed, nbytes)
+    hb = HostBatcher(device=0, chunk_bytes=1 << 20, nstreams=3)
+    out = hb.run(arena, lay.off, lay.length, lay.seed, complement=True)
+    expect = oracle.batch(arena, lay.off, lay.length, lay.seed, complement=True)
+    assert np.array_equal(out, expect)
+    # descriptors that violate the host API contract are rejected before any copy
+    with pytest.raises(_lib.ChecksumError):
+        hb.run(arena, lay.off[::-1].copy(), lay.length, None)
+    hb.close()
+    if pinned:
+        pb.free()
