@@ -80,7 +80,7 @@ _SIGNATURES = {
     "rns_compute_pseudo_header_checksum": (_i32, [ctypes.POINTER(RnsIpAddr), ctypes.POINTER(RnsIpAddr), _u64, _u8]),
     "rns_csum_batch_dev": (_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp]),
     "rns_csum_batch_strided_dev": (_int, [_vp, _u64, _u64, _u64, _u32, _vp, _vp, _u32, _u32, _vp, _vp]),
-    "rns_csum_batch_dev_cfg": (_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _vp, _vp]),
+    "rns_csum_batch_dev_cfg": (_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _u32, _vp, _vp]),
     "rns_host_ctx_create": (_int, [_int, _u64, _u32, ctypes.POINTER(_vp)]),
     "rns_host_ctx_destroy": (_int, [_vp]),
     "rns_csum_batch_host": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32]),
@@ -99,6 +99,14 @@ def load() -> ctypes.CDLL:
     global _LIB
     with _LOCK:
         if _LIB is None:
+            # PyTorch-ROCm bundles its own libamdhip64 (SONAME libamdhip64.so.7).  Importing
+            # torch first makes the dynamic linker bind this library to that same runtime, so
+            # the process has ONE HIP runtime and torch's streams / events / allocations are
+            # valid here.  (Loading ours first would pull /opt/rocm's runtime under torch.)
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
             if not os.path.exists(LIB_PATH):
                 raise ChecksumLibraryMissing(f"{LIB_PATH} not found; run __graft_entry__.build()")
             lib = ctypes.CDLL(LIB_PATH)

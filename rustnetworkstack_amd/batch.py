@@ -44,13 +44,13 @@ def _stream_handle(device: torch.device) -> int:
 
 def csum_batch(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, seed: torch.Tensor | None = None,
                *, complement: bool = False, out: torch.Tensor | None = None, len_hint: int = 0,
-               bad: torch.Tensor | None = None, shape: tuple[int, int, int] | None = None) -> torch.Tensor:
+               bad: torch.Tensor | None = None, shape: tuple[int, int, int, int] | None = None) -> torch.Tensor:
     """Checksum every packet of a device-resident batch; returns uint16 [n] on the same device.
 
     Launches on the current torch stream of ``arena``'s device and returns
     without synchronising.  A packet outside the arena yields 0 and increments
-    ``bad`` (int32 [1] device tensor) if given.  ``shape`` = (lanes_per_packet,
-    unroll, max_blocks) overrides the kernel shape (tuning).
+    ``bad`` (int32 [1] device tensor) if given.  ``shape`` = (variant,
+    lanes_per_packet, unroll, max_blocks) overrides the kernel shape (tuning).
     """
     _require_cuda(arena, "arena", (torch.uint8,))
     _require_cuda(off, "off", (torch.int64,))
@@ -90,9 +90,9 @@ def csum_batch(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, see
             st = lib.rns_csum_batch_dev(arena.data_ptr(), arena.numel(), off.data_ptr(), length.data_ptr(),
                                         seed_ptr, out.data_ptr(), n, flags, int(len_hint), bad_ptr, stream)
         else:
-            g, u, mb = shape
+            var, g, u, mb = shape
             st = lib.rns_csum_batch_dev_cfg(arena.data_ptr(), arena.numel(), off.data_ptr(), length.data_ptr(),
-                                            seed_ptr, out.data_ptr(), n, flags, g, u, mb, bad_ptr, stream)
+                                            seed_ptr, out.data_ptr(), n, flags, var, g, u, mb, bad_ptr, stream)
     _lib.check(st, "rns_csum_batch_dev")
     return out
 

@@ -158,6 +158,195 @@ __global__ __launch_bounds__(kBlock) void csum_batch_kernel(const CsumArgs a)
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// v2: "rounds" kernel — a wavefront owns 64 CONSECUTIVE packets (a batch).
+//
+//   * one coalesced load of the batch's 64 descriptors (lane l: packet base+l);
+//   * the batch is processed in G rounds; in round r, group g (G lanes) takes
+//     packet base + r*P + g (P = 64/G packets at once), its descriptor
+//     broadcast from lane r*P + g (readlane for G = 64, ds_bpermute otherwise);
+//   * the first pass (G*U chunks) of round r+1 is loaded BEFORE round r is
+//     consumed, so every wave keeps a pass of loads in flight while it masks,
+//     dot4-sums and reduces;
+//   * group sums use DPP (quad_perm, row_half_mirror, row_mirror) + ds_swizzle;
+//     lane l collects the sum of ITS packet, adds the seed, folds, and the 64
+//     results leave in ONE 128-byte store.  (v1's one-lane 2-byte stores from
+//     many CUs made small-packet batches write-bound: ~4 packets/ns.)
+// ---------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v)
+{
+    return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), CTRL, 0xF, 0xF, true));
+}
+
+// Sum over aligned groups of G lanes; every lane of a group receives its group's sum.
+template <int G>
+__device__ __forceinline__ uint32_t group_allreduce(uint32_t v)
+{
+    if constexpr (G >= 2) v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]: lane ^ 1
+    if constexpr (G >= 4) v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]: lane ^ 2
+    if constexpr (G >= 8) v += dpp_mov<0x141>(v);   // row_half_mirror: the other quad of 8
+    if constexpr (G >= 16) v += dpp_mov<0x140>(v);  // row_mirror: the other half of 16
+    if constexpr (G >= 32)                          // ds_swizzle bitmode xor 0x10: lane ^ 16
+        v += static_cast<uint32_t>(__builtin_amdgcn_ds_swizzle(static_cast<int>(v), 0x401F));
+    if constexpr (G >= 64)
+        v = __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 32);
+    return v;
+}
+
+template <int G>
+__device__ __forceinline__ uint32_t bcast_from(uint32_t v, uint32_t src)
+{
+    if constexpr (G == 64)
+        return __builtin_amdgcn_readlane(v, src);  // src is wave-uniform
+    else
+        return static_cast<uint32_t>(__shfl(static_cast<int>(v), static_cast<int>(src), 64));
+}
+
+struct Pkt {
+    const uint8_t *base;  // 16-byte aligned chunk base
+    uint32_t nch;         // chunks covering the packet (0 for an empty packet)
+    int s;                // first valid byte in chunk 0
+    int e;                // bytes valid in the last chunk (1..16)
+    uint32_t w_hi;        // dot4 weights picking the BE-high bytes
+};
+
+template <int G>
+__device__ __forceinline__ Pkt fetch_pkt(const CsumArgs &a, uint64_t d_start, uint32_t d_len, uint32_t src)
+{
+    const uint32_t lo = bcast_from<G>(static_cast<uint32_t>(d_start), src);
+    const uint32_t hi = bcast_from<G>(static_cast<uint32_t>(d_start >> 32), src);
+    const uint32_t L = bcast_from<G>(d_len, src);
+    const uint64_t start = (static_cast<uint64_t>(hi) << 32) | lo;
+    Pkt k;
+    k.s = static_cast<int>(start & 15);
+    k.base = a.arena + (start - static_cast<uint64_t>(k.s));
+    const uint64_t span = static_cast<uint64_t>(k.s) + L;
+    k.nch = L ? static_cast<uint32_t>((span + 15) >> 4) : 0u;
+    k.e = static_cast<int>(span - (static_cast<uint64_t>(k.nch ? k.nch - 1 : 0) << 4));
+    k.w_hi = (start & 1) ? 0x01000100u : 0x00010001u;
+    return k;
+}
+
+template <int G, int U>
+__device__ __forceinline__ void issue_pass(const Pkt &k, uint32_t c0, uint4 (&v)[U])
+{
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t c = c0 + u * G;
+        v[u] = (c < k.nch) ? *reinterpret_cast<const uint4 *>(k.base + (static_cast<uint64_t>(c) << 4))
+                           : make_uint4(0, 0, 0, 0);
+    }
+}
+
+template <int G, int U>
+__device__ __forceinline__ void consume_pass(const Pkt &k, uint32_t c0, uint4 (&v)[U], uint32_t &hs, uint32_t &ls)
+{
+    const uint32_t w_lo = k.w_hi ^ 0x01010101u;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t c = c0 + u * G;
+        if (c == 0 || c + 1 == k.nch) {
+            const int lo = (c == 0) ? k.s : 0;
+            const int hi = (c + 1 == k.nch) ? k.e : 16;
+            v[u].x = keep_bytes(v[u].x, lo, hi, 0);
+            v[u].y = keep_bytes(v[u].y, lo, hi, 4);
+            v[u].z = keep_bytes(v[u].z, lo, hi, 8);
+            v[u].w = keep_bytes(v[u].w, lo, hi, 12);
+        }
+        hs = __builtin_amdgcn_udot4(v[u].x, k.w_hi, hs, false);
+        ls = __builtin_amdgcn_udot4(v[u].x, w_lo, ls, false);
+        hs = __builtin_amdgcn_udot4(v[u].y, k.w_hi, hs, false);
+        ls = __builtin_amdgcn_udot4(v[u].y, w_lo, ls, false);
+        hs = __builtin_amdgcn_udot4(v[u].z, k.w_hi, hs, false);
+        ls = __builtin_amdgcn_udot4(v[u].z, w_lo, ls, false);
+        hs = __builtin_amdgcn_udot4(v[u].w, k.w_hi, hs, false);
+        ls = __builtin_amdgcn_udot4(v[u].w, w_lo, ls, false);
+    }
+}
+
+template <int G, int U, bool STRIDED>
+__global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
+{
+    static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two in [4,64]");
+    constexpr uint32_t P = 64 / G;        // packets per round
+    constexpr uint32_t kPass = G * U;     // chunks per pass
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t sub = lane & (G - 1);
+    const uint32_t grp = lane / G;
+    const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
+
+    for (uint64_t base = static_cast<uint64_t>(wave) * 64; base < a.n; base += static_cast<uint64_t>(nwaves) * 64) {
+        const uint64_t p = base + lane;
+        const bool live = p < a.n;
+        uint64_t d_start = 0;
+        uint32_t d_len = 0, d_seed = 0;
+        if (live) {
+            if constexpr (STRIDED) {
+                d_start = a.first_off + p * a.stride;
+                d_len = a.fixed_len;
+            } else {
+                d_start = a.off[p];
+                d_len = a.len[p];
+            }
+            d_seed = a.seed ? a.seed[p] : 0u;
+        }
+        d_start += a.base_adjust;
+        const bool d_ok = d_start <= a.arena_bytes && d_len <= a.arena_bytes - d_start;
+        if (!d_ok)
+            d_len = 0;
+
+        uint32_t mine = 0;  // BE-word sum (mod 2^32) of this lane's packet
+        Pkt cur = fetch_pkt<G>(a, d_start, d_len, grp);
+        uint4 v[U];
+        issue_pass<G, U>(cur, sub, v);
+        for (uint32_t r = 0; r < G; ++r) {
+            Pkt nxt = cur;
+            uint4 w[U];
+            if (r + 1 < G) {  // prefetch the next round's first pass
+                nxt = fetch_pkt<G>(a, d_start, d_len, (r + 1) * P + grp);
+                issue_pass<G, U>(nxt, sub, w);
+            }
+            uint32_t hs = 0, ls = 0;
+            consume_pass<G, U>(cur, sub, v, hs, ls);
+            for (uint32_t c0 = kPass + sub; c0 < cur.nch; c0 += kPass) {  // packets longer than one pass
+                uint4 x[U];
+                issue_pass<G, U>(cur, c0, x);
+                consume_pass<G, U>(cur, c0, x, hs, ls);
+            }
+            const uint32_t words = group_allreduce<G>((hs << 8) + ls);
+            if constexpr (G == 64) {
+                mine = (lane == r) ? words : mine;
+            } else {
+                const uint32_t t = bcast_from<G>(words, (lane % P) * G);  // group (lane % P)'s sum
+                mine = (lane / P == r) ? t : mine;
+            }
+            if (r + 1 < G) {
+                cur = nxt;
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    v[u] = w[u];
+            }
+        }
+        uint32_t acc = d_seed + mine;  // util.rs:89-99 (mod 2^32)
+        while (acc > 0xffff)           // util.rs:101-103
+            acc = (acc & 0xffff) + (acc >> 16);
+        if (a.flags & RNS_FLAG_COMPLEMENT)
+            acc ^= 0xffff;
+        if (!d_ok)
+            acc = 0;
+        if (live)
+            a.out[p] = static_cast<uint16_t>(acc);  // 64 consecutive u16: one 128-byte store
+        if (a.bad) {
+            const uint64_t rejected = __ballot(live && !d_ok);
+            if (rejected && lane == 0)
+                atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
+        }
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void splitmix64_fill_kernel(uint8_t *buf, uint64_t nbytes, uint64_t seed)
 {
     const uint64_t nwords = (nbytes + 7) / 8;
@@ -178,42 +367,57 @@ __global__ __launch_bounds__(kBlock) void splitmix64_fill_kernel(uint8_t *buf, u
 
 inline int hip_status(hipError_t e) { return e == hipSuccess ? RNS_OK : RNS_E_HIP_BASE - static_cast<int>(e); }
 
+// Kernel variants: 0 = v1 group kernel (one lane stores each result), 1 = v2 rounds kernel.
 template <int G, int U, bool S>
-int launch_shape(const CsumArgs &a, uint32_t max_blocks, hipStream_t st)
+int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipStream_t st)
 {
-    constexpr uint32_t kGroups = kBlock / G;
-    uint64_t blocks = (static_cast<uint64_t>(a.n) + kGroups - 1) / kGroups;
+    uint64_t blocks;
+    if (variant == 0) {
+        constexpr uint32_t kGroups = kBlock / G;
+        blocks = (static_cast<uint64_t>(a.n) + kGroups - 1) / kGroups;
+    } else {
+        const uint64_t batches = (static_cast<uint64_t>(a.n) + 63) / 64;  // one wave per 64 packets
+        blocks = (batches + kBlock / 64 - 1) / (kBlock / 64);
+    }
     if (max_blocks != 0 && blocks > max_blocks)
         blocks = max_blocks;
     if (blocks == 0)
         return RNS_OK;
-    hipLaunchKernelGGL((csum_batch_kernel<G, U, S>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, st, a);
+    if (variant == 0)
+        hipLaunchKernelGGL((csum_batch_kernel<G, U, S>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, st, a);
+    else
+        hipLaunchKernelGGL((csum_rounds_kernel<G, U, S>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, st, a);
     return hip_status(hipGetLastError());
 }
 
 template <bool S>
-int dispatch(const CsumArgs &a, uint32_t G, uint32_t U, uint32_t max_blocks, hipStream_t st)
+int dispatch(const CsumArgs &a, uint32_t variant, uint32_t G, uint32_t U, uint32_t max_blocks, hipStream_t st)
 {
+    if (variant > 1)
+        return RNS_E_INVALID;
 #define RNS_SHAPE(g, u) \
-    if (G == g && U == u) return launch_shape<g, u, S>(a, max_blocks, st);
-    RNS_SHAPE(4, 1) RNS_SHAPE(4, 2) RNS_SHAPE(4, 4)
-    RNS_SHAPE(8, 1) RNS_SHAPE(8, 2) RNS_SHAPE(8, 4)
-    RNS_SHAPE(16, 1) RNS_SHAPE(16, 2) RNS_SHAPE(16, 4)
-    RNS_SHAPE(32, 1) RNS_SHAPE(32, 2) RNS_SHAPE(32, 4)
-    RNS_SHAPE(64, 1) RNS_SHAPE(64, 2) RNS_SHAPE(64, 4)
+    if (G == g && U == u) return launch_shape<g, u, S>(a, variant, max_blocks, st);
+    RNS_SHAPE(4, 1) RNS_SHAPE(4, 2) RNS_SHAPE(4, 4) RNS_SHAPE(4, 8)
+    RNS_SHAPE(8, 1) RNS_SHAPE(8, 2) RNS_SHAPE(8, 4) RNS_SHAPE(8, 8)
+    RNS_SHAPE(16, 1) RNS_SHAPE(16, 2) RNS_SHAPE(16, 4) RNS_SHAPE(16, 8)
+    RNS_SHAPE(32, 1) RNS_SHAPE(32, 2) RNS_SHAPE(32, 4) RNS_SHAPE(32, 8)
+    RNS_SHAPE(64, 1) RNS_SHAPE(64, 2) RNS_SHAPE(64, 4) RNS_SHAPE(64, 8)
 #undef RNS_SHAPE
     return RNS_E_INVALID;
 }
 
-// Lanes per packet and chunks in flight per lane for a typical packet length.
-void pick_shape(uint32_t len_hint, uint32_t *G, uint32_t *U)
+// Kernel shape for a typical packet length (chunks of 16 B a packet spans).
+struct Shape {
+    uint32_t variant, G, U, max_blocks;
+};
+
+Shape pick_shape(uint32_t len_hint)
 {
     const uint32_t chunks = len_hint ? (len_hint + 15) / 16 + 1 : 96;
     uint32_t g = 4;
-    while (g < 64 && g * 2 < chunks)
+    while (g < 64 && g * 4 < chunks)
         g *= 2;
-    *G = g;
-    *U = (chunks > 2 * g) ? 4 : 2;
+    return Shape{1u, g, chunks > 2 * g ? 4u : 2u, 0u};
 }
 
 int check_device()
@@ -299,7 +503,7 @@ extern "C" {
 
 int rns_csum_batch_dev_cfg(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off,
                            const uint32_t *d_len, const uint16_t *d_seed, uint16_t *d_out, uint32_t n,
-                           uint32_t flags, uint32_t lanes_per_packet, uint32_t unroll,
+                           uint32_t flags, uint32_t variant, uint32_t lanes_per_packet, uint32_t unroll,
                            uint32_t max_blocks, uint32_t *d_bad, void *stream)
 {
     if (n == 0)
@@ -317,17 +521,16 @@ int rns_csum_batch_dev_cfg(const uint8_t *d_arena, uint64_t arena_bytes, const u
     a.bad = d_bad;
     a.n = n;
     a.flags = flags;
-    return dispatch<false>(a, lanes_per_packet, unroll, max_blocks, static_cast<hipStream_t>(stream));
+    return dispatch<false>(a, variant, lanes_per_packet, unroll, max_blocks, static_cast<hipStream_t>(stream));
 }
 
 int rns_csum_batch_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off,
                        const uint32_t *d_len, const uint16_t *d_seed, uint16_t *d_out, uint32_t n,
                        uint32_t flags, uint32_t len_hint, uint32_t *d_bad, void *stream)
 {
-    uint32_t G, U;
-    pick_shape(len_hint, &G, &U);
-    return rns_csum_batch_dev_cfg(d_arena, arena_bytes, d_off, d_len, d_seed, d_out, n, flags, G, U, 0,
-                                  d_bad, stream);
+    const Shape sh = pick_shape(len_hint);
+    return rns_csum_batch_dev_cfg(d_arena, arena_bytes, d_off, d_len, d_seed, d_out, n, flags, sh.variant, sh.G,
+                                  sh.U, sh.max_blocks, d_bad, stream);
 }
 
 int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uint64_t first_off,
@@ -350,9 +553,8 @@ int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uin
     a.fixed_len = len;
     a.n = n;
     a.flags = flags;
-    uint32_t G, U;
-    pick_shape(len, &G, &U);
-    return dispatch<true>(a, G, U, 0, static_cast<hipStream_t>(stream));
+    const Shape sh = pick_shape(len);
+    return dispatch<true>(a, sh.variant, sh.G, sh.U, sh.max_blocks, static_cast<hipStream_t>(stream));
 }
 
 int rns_host_ctx_create(int device, uint64_t chunk_bytes, uint32_t nstreams, rns_host_ctx **out)
@@ -468,9 +670,8 @@ int rns_csum_batch_host(rns_host_ctx *ctx, const uint8_t *h_arena, uint64_t aren
         a.out = s.d_out;
         a.n = cnt;
         a.flags = flags;
-        uint32_t G, U;
-        pick_shape(static_cast<uint32_t>(std::min<uint64_t>((hi - lo) / cnt, 1u << 30)), &G, &U);
-        st = dispatch<false>(a, G, U, 0, s.stream);
+        const Shape sh = pick_shape(static_cast<uint32_t>(std::min<uint64_t>((hi - lo) / cnt, 1u << 30)));
+        st = dispatch<false>(a, sh.variant, sh.G, sh.U, sh.max_blocks, s.stream);
         if (st)
             break;
         e = hipMemcpyAsync(s.h_out, s.d_out, cnt * sizeof(uint16_t), hipMemcpyDeviceToHost, s.stream);

@@ -1,0 +1,64 @@
+"""Kernel-shape sweep on one GPU: average device time per launch (HIP events on the
+launch stream), interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24).
+
+    python tools/sweep_shapes.py [--configs c3_1500B,...] [--rounds 5] [--iters 10]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from rustnetworkstack_amd.workloads import DeviceBatch, make_layout  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c3_1500B,c4_9000B,c2_64B,c5_imix")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--shapes", default="")
+    args = ap.parse_args()
+    if args.shapes:
+        shapes = [tuple(int(x) for x in s.split(",")) for s in args.shapes.split(";")]
+    else:
+        shapes = [(0, 16, 2, 0), (0, 64, 4, 0), (0, 8, 4, 0)]
+        shapes += [(1, g, u, mb) for g in (4, 8, 16, 32, 64) for u in (1, 2, 4, 8) for mb in (0, 2048)]
+    results = {}
+    for cfg in args.configs.split(","):
+        lay = make_layout(cfg)
+        b = DeviceBatch(lay, "cuda:0")
+        b.run()
+        ref = b.host_out()
+        times = {s: [] for s in shapes}
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.iters)]
+        for _ in range(args.rounds):
+            for s in shapes:
+                b.run(shape=s)
+                for i in range(args.iters):
+                    ev[i][0].record()
+                    b.run(shape=s)
+                    ev[i][1].record()
+                torch.cuda.synchronize()
+                times[s].append(sum(a.elapsed_time(e) for a, e in ev) / args.iters)
+                assert (b.host_out() == ref).all(), s
+        algo = lay.payload_bytes + 2 * lay.n
+        rows = []
+        for s in shapes:
+            t = sorted(times[s])
+            med = t[len(t) // 2]
+            rows.append((med, s, algo / (med * 1e-3) / 1e9, t[0]))
+        rows.sort()
+        results[cfg] = [{"shape": list(s), "median_us": round(m * 1e3, 1), "min_us": round(mn * 1e3, 1),
+                         "GBps": round(gbs, 1)} for m, s, gbs, mn in rows]
+        print(cfg, json.dumps(results[cfg][:8]), flush=True)
+        del b
+        torch.cuda.empty_cache()
+    print(json.dumps(results))
+
+
+if __name__ == "__main__":
+    main()
