@@ -42,6 +42,73 @@ def _stream_handle(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+class PreparedBatch:
+    """A device-resident batch bound to the C ABI once: validation and argument
+    marshalling happen here, so each launch is a single ctypes call (a few µs of
+    host time).  Launches go to the stream that was current at construction.
+
+    ``shape`` = (variant, lanes_per_packet, unroll, max_blocks) overrides the
+    automatic kernel shape (tuning); see rns_csum_batch_dev_cfg.
+    """
+
+    def __init__(self, arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor,
+                 seed: torch.Tensor | None = None, *, complement: bool = False, out: torch.Tensor | None = None,
+                 len_hint: int = 0, bad: torch.Tensor | None = None,
+                 shape: tuple[int, int, int, int] | None = None):
+        _require_cuda(arena, "arena", (torch.uint8,))
+        _require_cuda(off, "off", (torch.int64,))
+        _require_cuda(length, "length", (torch.int32,))
+        n = off.numel()
+        if length.numel() != n:
+            raise ValueError("off and length must have the same number of packets")
+        if n >= 2 ** 32:
+            raise ValueError("at most 2^32-1 packets per call")
+        dev = arena.device
+        for name, t in (("off", off), ("length", length)):
+            if t.device != dev:
+                raise ValueError(f"{name} is on {t.device}, arena on {dev}")
+        seed_ptr = None
+        if seed is not None:
+            _require_cuda(seed, "seed", _U16)
+            if seed.numel() != n or seed.device != dev:
+                raise ValueError("seed must have one entry per packet on the arena's device")
+            seed_ptr = seed.data_ptr()
+        if out is None:
+            out = torch.empty(n, dtype=torch.uint16, device=dev)
+        else:
+            _require_cuda(out, "out", _U16)
+            if out.numel() != n or out.device != dev:
+                raise ValueError("out must have one entry per packet on the arena's device")
+        bad_ptr = None
+        if bad is not None:
+            _require_cuda(bad, "bad", (torch.int32,))
+            bad_ptr = bad.data_ptr()
+        lib = _lib.load()
+        flags = _lib.RNS_FLAG_COMPLEMENT if complement else 0
+        stream = _stream_handle(dev)
+        # keep the tensors alive as long as the bound pointers
+        self._keep = (arena, off, length, seed, out, bad)
+        self.out = out
+        self.n = n
+        self.device = dev
+        if shape is None:
+            self._fn = lib.rns_csum_batch_dev
+            self._args = (arena.data_ptr(), arena.numel(), off.data_ptr(), length.data_ptr(), seed_ptr,
+                          out.data_ptr(), n, flags, int(len_hint), bad_ptr, stream)
+        else:
+            var, g, u, mb = shape
+            self._fn = lib.rns_csum_batch_dev_cfg
+            self._args = (arena.data_ptr(), arena.numel(), off.data_ptr(), length.data_ptr(), seed_ptr,
+                          out.data_ptr(), n, flags, var, g, u, mb, bad_ptr, stream)
+
+    def __call__(self) -> torch.Tensor:
+        if self.n:
+            st = self._fn(*self._args)
+            if st != _lib.RNS_OK:
+                raise _lib.ChecksumError(st, "rns_csum_batch_dev")
+        return self.out
+
+
 def csum_batch(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, seed: torch.Tensor | None = None,
                *, complement: bool = False, out: torch.Tensor | None = None, len_hint: int = 0,
                bad: torch.Tensor | None = None, shape: tuple[int, int, int, int] | None = None) -> torch.Tensor:
@@ -52,49 +119,9 @@ def csum_batch(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, see
     ``bad`` (int32 [1] device tensor) if given.  ``shape`` = (variant,
     lanes_per_packet, unroll, max_blocks) overrides the kernel shape (tuning).
     """
-    _require_cuda(arena, "arena", (torch.uint8,))
-    _require_cuda(off, "off", (torch.int64,))
-    _require_cuda(length, "length", (torch.int32,))
-    n = off.numel()
-    if length.numel() != n:
-        raise ValueError("off and length must have the same number of packets")
-    if n >= 2 ** 32:
-        raise ValueError("at most 2^32-1 packets per call")
-    dev = arena.device
-    for name, t in (("off", off), ("length", length)):
-        if t.device != dev:
-            raise ValueError(f"{name} is on {t.device}, arena on {dev}")
-    seed_ptr = None
-    if seed is not None:
-        _require_cuda(seed, "seed", _U16)
-        if seed.numel() != n or seed.device != dev:
-            raise ValueError("seed must have one entry per packet on the arena's device")
-        seed_ptr = seed.data_ptr()
-    if out is None:
-        out = torch.empty(n, dtype=torch.uint16, device=dev)
-    else:
-        _require_cuda(out, "out", _U16)
-        if out.numel() != n or out.device != dev:
-            raise ValueError("out must have one entry per packet on the arena's device")
-    bad_ptr = None
-    if bad is not None:
-        _require_cuda(bad, "bad", (torch.int32,))
-        bad_ptr = bad.data_ptr()
-    if n == 0:
-        return out
-    lib = _lib.load()
-    flags = _lib.RNS_FLAG_COMPLEMENT if complement else 0
-    with torch.cuda.device(dev):
-        stream = _stream_handle(dev)
-        if shape is None:
-            st = lib.rns_csum_batch_dev(arena.data_ptr(), arena.numel(), off.data_ptr(), length.data_ptr(),
-                                        seed_ptr, out.data_ptr(), n, flags, int(len_hint), bad_ptr, stream)
-        else:
-            var, g, u, mb = shape
-            st = lib.rns_csum_batch_dev_cfg(arena.data_ptr(), arena.numel(), off.data_ptr(), length.data_ptr(),
-                                            seed_ptr, out.data_ptr(), n, flags, var, g, u, mb, bad_ptr, stream)
-    _lib.check(st, "rns_csum_batch_dev")
-    return out
+    with torch.cuda.device(arena.device if arena.is_cuda else None):
+        return PreparedBatch(arena, off, length, seed, complement=complement, out=out, len_hint=len_hint, bad=bad,
+                             shape=shape)()
 
 
 def csum_batch_strided(arena: torch.Tensor, n: int, stride: int, length: int, *, first_off: int = 0,

@@ -54,6 +54,21 @@ struct CsumArgs {
     uint32_t flags;
 };
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// One 16-byte chunk.  NT = nontemporal (streamed once: do not keep it in the
+// caches; the HBM read probe in tools/ measured +5..10 % for streaming reads).
+template <bool NT>
+__device__ __forceinline__ uint4 load_chunk(const uint8_t *p)
+{
+    if constexpr (NT) {
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *reinterpret_cast<const uint4 *>(p);
+    }
+}
+
 // Keep bytes [lo, hi) of the 4-byte dword at byte j4 = 4*j of a 16-byte chunk.
 __device__ __forceinline__ uint32_t keep_bytes(uint32_t d, int lo, int hi, int j4)
 {
@@ -73,7 +88,7 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t v)
     return v;
 }
 
-template <int G, int U, bool STRIDED>
+template <int G, int U, bool STRIDED, bool NT>
 __global__ __launch_bounds__(kBlock) void csum_batch_kernel(const CsumArgs a)
 {
     static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two in [4,64]");
@@ -112,7 +127,7 @@ __global__ __launch_bounds__(kBlock) void csum_batch_kernel(const CsumArgs a)
                 for (int u = 0; u < U; ++u) {
                     const uint32_t c = c0 + u * G;
                     if (c < nch)
-                        v[u] = *reinterpret_cast<const uint4 *>(base + (static_cast<uint64_t>(c) << 4));
+                        v[u] = load_chunk<NT>(base + (static_cast<uint64_t>(c) << 4));
                     else
                         v[u] = make_uint4(0, 0, 0, 0);
                 }
@@ -229,14 +244,13 @@ __device__ __forceinline__ Pkt fetch_pkt(const CsumArgs &a, uint64_t d_start, ui
     return k;
 }
 
-template <int G, int U>
+template <int G, int U, bool NT>
 __device__ __forceinline__ void issue_pass(const Pkt &k, uint32_t c0, uint4 (&v)[U])
 {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t c = c0 + u * G;
-        v[u] = (c < k.nch) ? *reinterpret_cast<const uint4 *>(k.base + (static_cast<uint64_t>(c) << 4))
-                           : make_uint4(0, 0, 0, 0);
+        v[u] = (c < k.nch) ? load_chunk<NT>(k.base + (static_cast<uint64_t>(c) << 4)) : make_uint4(0, 0, 0, 0);
     }
 }
 
@@ -266,7 +280,7 @@ __device__ __forceinline__ void consume_pass(const Pkt &k, uint32_t c0, uint4 (&
     }
 }
 
-template <int G, int U, bool STRIDED>
+template <int G, int U, bool STRIDED, bool NT>
 __global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
 {
     static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two in [4,64]");
@@ -301,19 +315,19 @@ __global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
         uint32_t mine = 0;  // BE-word sum (mod 2^32) of this lane's packet
         Pkt cur = fetch_pkt<G>(a, d_start, d_len, grp);
         uint4 v[U];
-        issue_pass<G, U>(cur, sub, v);
+        issue_pass<G, U, NT>(cur, sub, v);
         for (uint32_t r = 0; r < G; ++r) {
             Pkt nxt = cur;
             uint4 w[U];
             if (r + 1 < G) {  // prefetch the next round's first pass
                 nxt = fetch_pkt<G>(a, d_start, d_len, (r + 1) * P + grp);
-                issue_pass<G, U>(nxt, sub, w);
+                issue_pass<G, U, NT>(nxt, sub, w);
             }
             uint32_t hs = 0, ls = 0;
             consume_pass<G, U>(cur, sub, v, hs, ls);
             for (uint32_t c0 = kPass + sub; c0 < cur.nch; c0 += kPass) {  // packets longer than one pass
                 uint4 x[U];
-                issue_pass<G, U>(cur, c0, x);
+                issue_pass<G, U, NT>(cur, c0, x);
                 consume_pass<G, U>(cur, c0, x, hs, ls);
             }
             const uint32_t words = group_allreduce<G>((hs << 8) + ls);
@@ -367,12 +381,12 @@ __global__ __launch_bounds__(kBlock) void splitmix64_fill_kernel(uint8_t *buf, u
 
 inline int hip_status(hipError_t e) { return e == hipSuccess ? RNS_OK : RNS_E_HIP_BASE - static_cast<int>(e); }
 
-// Kernel variants: 0 = v1 group kernel (one lane stores each result), 1 = v2 rounds kernel.
+// Kernel variants: bit 0 = rounds kernel (1) / group kernel (0); bit 1 = nontemporal loads.
 template <int G, int U, bool S>
 int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipStream_t st)
 {
     uint64_t blocks;
-    if (variant == 0) {
+    if ((variant & 1) == 0) {
         constexpr uint32_t kGroups = kBlock / G;
         blocks = (static_cast<uint64_t>(a.n) + kGroups - 1) / kGroups;
     } else {
@@ -383,17 +397,20 @@ int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipSt
         blocks = max_blocks;
     if (blocks == 0)
         return RNS_OK;
-    if (variant == 0)
-        hipLaunchKernelGGL((csum_batch_kernel<G, U, S>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, st, a);
-    else
-        hipLaunchKernelGGL((csum_rounds_kernel<G, U, S>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, st, a);
+    const dim3 grid(static_cast<uint32_t>(blocks)), block(kBlock);
+    switch (variant) {
+    case 0: hipLaunchKernelGGL((csum_batch_kernel<G, U, S, false>), grid, block, 0, st, a); break;
+    case 1: hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, false>), grid, block, 0, st, a); break;
+    case 2: hipLaunchKernelGGL((csum_batch_kernel<G, U, S, true>), grid, block, 0, st, a); break;
+    default: hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true>), grid, block, 0, st, a); break;
+    }
     return hip_status(hipGetLastError());
 }
 
 template <bool S>
 int dispatch(const CsumArgs &a, uint32_t variant, uint32_t G, uint32_t U, uint32_t max_blocks, hipStream_t st)
 {
-    if (variant > 1)
+    if (variant > 3)
         return RNS_E_INVALID;
 #define RNS_SHAPE(g, u) \
     if (G == g && U == u) return launch_shape<g, u, S>(a, variant, max_blocks, st);

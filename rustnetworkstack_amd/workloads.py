@@ -17,7 +17,7 @@ c5_imix   2^23 IMIX 40/576/1500  8 GPU mixed sizes, sharded by packet index
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 
@@ -55,14 +55,14 @@ class Layout:
     seed: np.ndarray     # uint16
     arena_bytes: int
     data_seed: int
+    payload_bytes: int = field(init=False)
+
+    def __post_init__(self):
+        self.payload_bytes = int(self.length.astype(np.uint64).sum())
 
     @property
     def n(self) -> int:
         return int(self.off.shape[0])
-
-    @property
-    def payload_bytes(self) -> int:
-        return int(self.length.astype(np.uint64).sum())
 
     @property
     def mean_len(self) -> float:
@@ -123,11 +123,19 @@ class DeviceBatch:
         self.length = torch.from_numpy(layout.length.view(np.int32)).to(self.device)
         self.seed = torch.from_numpy(layout.seed.view(np.int16)).to(self.device)
         self.out = torch.empty(layout.n, dtype=torch.uint16, device=self.device)
+        self._prepared = {}
+
+    def launcher(self, complement: bool = False, shape=None):
+        """Pre-bound launch (one ctypes call per launch) on the current stream."""
+        from .batch import PreparedBatch
+        key = (complement, shape)
+        if key not in self._prepared:
+            self._prepared[key] = PreparedBatch(self.arena, self.off, self.length, self.seed, complement=complement,
+                                                out=self.out, len_hint=int(round(self.layout.mean_len)), shape=shape)
+        return self._prepared[key]
 
     def run(self, complement: bool = False, shape=None):
-        from .batch import csum_batch
-        return csum_batch(self.arena, self.off, self.length, self.seed, complement=complement, out=self.out,
-                          len_hint=int(round(self.layout.mean_len)), shape=shape)
+        return self.launcher(complement, shape)()
 
     def host_arena(self) -> np.ndarray:
         return self.arena.cpu().numpy()
