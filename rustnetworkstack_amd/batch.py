@@ -119,7 +119,8 @@ def csum_batch(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, see
     ``bad`` (int32 [1] device tensor) if given.  ``shape`` = (variant,
     lanes_per_packet, unroll, max_blocks) overrides the kernel shape (tuning).
     """
-    with torch.cuda.device(arena.device if arena.is_cuda else None):
+    _require_cuda(arena, "arena", (torch.uint8,))
+    with torch.cuda.device(arena.device):
         return PreparedBatch(arena, off, length, seed, complement=complement, out=out, len_hint=len_hint, bad=bad,
                              shape=shape)()
 
