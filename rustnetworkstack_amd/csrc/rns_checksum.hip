@@ -423,7 +423,13 @@ int dispatch(const CsumArgs &a, uint32_t variant, uint32_t G, uint32_t U, uint32
     return RNS_E_INVALID;
 }
 
-// Kernel shape for a typical packet length (chunks of 16 B a packet spans).
+// Kernel shape for a typical packet length (chunks of 16 B a packet spans),
+// from the interleaved shape sweep on MI355X (tools/sweep_shapes.py,
+// profiles/r01_sweep.json):
+//   <= 8 chunks  (64 B)    rounds, nontemporal, G=4,  U=1, grid 2048  (c2)
+//   <= 48 chunks (IMIX)    rounds,              G=4,  U=4             (c5: mixed 40/576/1500 B)
+//   <= 160 chunks (1500 B) rounds, nontemporal, G=32, U=4             (c3, headline)
+//   longer (9000 B)        group,  nontemporal, G=64, U=4             (c4)
 struct Shape {
     uint32_t variant, G, U, max_blocks;
 };
@@ -431,10 +437,13 @@ struct Shape {
 Shape pick_shape(uint32_t len_hint)
 {
     const uint32_t chunks = len_hint ? (len_hint + 15) / 16 + 1 : 96;
-    uint32_t g = 4;
-    while (g < 64 && g * 4 < chunks)
-        g *= 2;
-    return Shape{1u, g, chunks > 2 * g ? 4u : 2u, 0u};
+    if (chunks <= 8)
+        return Shape{3u, 4u, 1u, 2048u};
+    if (chunks <= 48)
+        return Shape{1u, 4u, 4u, 0u};
+    if (chunks <= 160)
+        return Shape{3u, 32u, 4u, 0u};
+    return Shape{2u, 64u, 4u, 0u};
 }
 
 int check_device()
@@ -739,7 +748,8 @@ int rns_fill_splitmix64_dev(uint8_t *d_buf, uint64_t nbytes, uint64_t seed, void
 
 const char *rns_build_info(void)
 {
-    return "rns_checksum abi=1 offload-arch=gfx950 kernel=csum_batch_kernel<G,U> (dot4 BE-half sums, wave64)";
+    return "rns_checksum abi=1 offload-arch=gfx950 kernels=csum_rounds_kernel/csum_batch_kernel<G,U,NT> "
+           "(dot4 BE-half sums, wave64, DPP group reduction)";
 }
 
 int rns_device_count(void)

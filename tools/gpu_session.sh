@@ -31,4 +31,13 @@ step bench 600 python bench.py "$@"
 cd /tmp
 step rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
      python3 "$ROOT/bench.py" --no-cpu-baseline --no-host-pipeline "$@"
+# HBM traffic: FETCH_SIZE and WRITE_SIZE in separate passes, counters only (no other trace domains)
+step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
+     python3 "$ROOT/bench.py" --no-cpu-baseline --no-host-pipeline --steps 5 --warmup 1
+step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
+     python3 "$ROOT/bench.py" --no-cpu-baseline --no-host-pipeline --steps 5 --warmup 1
+cd "$ROOT"
+python tools/pmc_traffic.py --fetch "$OUT/pmc_fetch" --write "$OUT/pmc_write" --config c3_1500B \
+     --kernel csum_ --algo-bytes 1574961152 --out "$OUT/traffic_c3_1500B.json" > "$OUT/traffic.log" 2>&1
+echo "traffic rc=$?"; cat "$OUT/traffic.log" | tail -3
 echo "== done"
