@@ -36,7 +36,7 @@ def parse_args(argv=None):
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="c3_1500B")
-    p.add_argument("--shape", default="", help="G,U,max_blocks kernel shape override (tuning)")
+    p.add_argument("--shape", default="", help="variant,G,U,max_blocks kernel shape override (tuning)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample duration (single thread)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-pipeline", action="store_true", help="skip the PCIe-inclusive extra measurement")
@@ -87,16 +87,19 @@ class Dist:
 
 def timed_loop(engine, dist: Dist, steps: int, warmup: int) -> dict:
     """W untimed steps, then exactly K steps bracketed by sync + barrier on both
-    sides; wall time is the max over ranks.  Per-launch device time comes from
-    events recorded on the launch stream."""
+    sides; wall time is the max over ranks.  Device time per launch = one pair of
+    events on the launch stream around the K back-to-back launches, / K (events
+    between launches would insert ~10 µs gaps: see DESIGN.md, measurement)."""
     for _ in range(warmup):
         engine.step()
     engine.sync()
     dist.barrier()
     engine.sync()
     t0 = time.perf_counter()
-    for i in range(steps):
-        engine.step(timed_index=i)
+    engine.begin_timing()
+    for _ in range(steps):
+        engine.step()
+    engine.end_timing(steps)
     engine.sync()
     dist.barrier()
     engine.sync()
@@ -127,8 +130,7 @@ class GpuEngine:
         self.shape = shape
         self.gather = gather_dist
         self.k = 0
-        self.ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                   for _ in range(max(steps, 1))]
+        self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         self.timed = 0
         if gather_dist is not None and gather_dist.enabled:
             n = self.layout.n
@@ -143,26 +145,31 @@ class GpuEngine:
     def payload_bytes(self):
         return self.layout.payload_bytes
 
-    def step(self, timed_index: int | None = None):
+    def step(self):
         b = self.batches[self.k % len(self.batches)]
         self.k += 1
-        launch = b.launcher(complement=True, shape=self.shape)  # pre-bound ctypes call
-        if timed_index is not None:
-            self.ev[timed_index][0].record()
-        launch()
-        if timed_index is not None:
-            self.ev[timed_index][1].record()
-            self.timed = timed_index + 1
+        b.launcher(complement=True, shape=self.shape)()  # pre-bound: one ctypes call
         if self.gather is not None and self.gather.enabled:
             self.gather.dist.all_gather_into_tensor(self.gathered, b.out.view(self.torch.int16))
 
     def sync(self):
         self.torch.cuda.synchronize()
 
+    def begin_timing(self):
+        self.ev[0].record()  # current stream = the stream every launch goes to
+
+    def end_timing(self, steps: int):
+        self.ev[1].record()
+        self.timed = steps
+
     def kernel_ms(self) -> float:
         if not self.timed:
             return float("nan")
-        return sum(a.elapsed_time(b) for a, b in self.ev[:self.timed]) / self.timed
+        return self.ev[0].elapsed_time(self.ev[1]) / self.timed
+
+    def kernel_name(self) -> str:
+        from rustnetworkstack_amd import _lib
+        return _lib.load().rns_csum_shape_name(int(round(self.layout.mean_len))).decode()
 
     def out_sample(self, count: int):
         import numpy as np
@@ -299,7 +306,7 @@ def main(argv=None):
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
-            "kernel": "csum_batch_kernel",
+            "kernel": engine.kernel_name() if shape is None else f"shape {list(shape)}",
             "kernel_avg_us": round(kernel_ms * 1e3, 2),
             "algorithmic_bytes_per_launch": algo_bytes,
             "traffic_source": (traffic or {}).get("source"),

@@ -151,6 +151,8 @@ int rns_fill_splitmix64_dev(uint8_t *d_buf, uint64_t nbytes, uint64_t seed, void
 int rns_abi_version(void);
 const char *rns_strerror(int status);
 const char *rns_build_info(void);
+/* Kernel and shape rns_csum_batch_dev picks for a typical packet length. */
+const char *rns_csum_shape_name(uint32_t len_hint);
 int rns_device_count(void);
 
 #ifdef __cplusplus

@@ -42,6 +42,7 @@ EXPORTED_SYMBOLS = (
     "rns_abi_version",
     "rns_strerror",
     "rns_build_info",
+    "rns_csum_shape_name",
     "rns_device_count",
 )
 
@@ -90,6 +91,7 @@ _SIGNATURES = {
     "rns_abi_version": (_int, []),
     "rns_strerror": (ctypes.c_char_p, [_int]),
     "rns_build_info": (ctypes.c_char_p, []),
+    "rns_csum_shape_name": (ctypes.c_char_p, [_u32]),
     "rns_device_count": (_int, []),
 }
 

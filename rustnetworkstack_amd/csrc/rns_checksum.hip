@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -744,6 +745,17 @@ int rns_fill_splitmix64_dev(uint8_t *d_buf, uint64_t nbytes, uint64_t seed, void
     hipLaunchKernelGGL(splitmix64_fill_kernel, dim3(blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
                        d_buf, nbytes, seed);
     return hip_status(hipGetLastError());
+}
+
+const char *rns_csum_shape_name(uint32_t len_hint)
+{
+    static const char *const names[] = {"csum_batch_kernel", "csum_rounds_kernel", "csum_batch_kernel[nt]",
+                                        "csum_rounds_kernel[nt]"};
+    static thread_local char buf[96];
+    const Shape sh = pick_shape(len_hint);
+    std::snprintf(buf, sizeof(buf), "%s<G=%u,U=%u>%s", names[sh.variant & 3], sh.G, sh.U,
+                  sh.max_blocks ? " grid-capped" : "");
+    return buf;
 }
 
 const char *rns_build_info(void)

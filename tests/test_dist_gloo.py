@@ -28,15 +28,16 @@ class CpuEngine:
         self.out = None
     n = property(lambda s: s.layout.n)
     payload_bytes = property(lambda s: s.layout.payload_bytes)
-    def step(self, timed_index=None):
-        t0 = time.perf_counter()
+    def step(self):
         self.out = self.orc.batch(self.arena, self.layout.off, self.layout.length, self.layout.seed, complement=True)
-        if timed_index is not None:
-            self.times.append(time.perf_counter() - t0)
     def sync(self):
         pass
+    def begin_timing(self):
+        self.t0 = time.perf_counter()
+    def end_timing(self, steps):
+        self.ms = 1e3 * (time.perf_counter() - self.t0) / steps
     def kernel_ms(self):
-        return 1e3 * sum(self.times) / len(self.times)
+        return self.ms
 
 d = bench.Dist(backend="gloo")
 eng = CpuEngine(d.rank, d.world)
