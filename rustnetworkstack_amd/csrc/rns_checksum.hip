@@ -220,45 +220,68 @@ __device__ __forceinline__ uint32_t bcast_from(uint32_t v, uint32_t src)
         return static_cast<uint32_t>(__shfl(static_cast<int>(v), static_cast<int>(src), 64));
 }
 
+// Packets up to this length cannot wrap the reference's u32 accumulator
+// (seed + 65537 words * 0xffff <= 2^32 - 1): they take the one-op-per-dword
+// v_sad_u16 path.  Longer packets take the exact dot4 path (wrap emulated).
+constexpr uint32_t kNoWrapBytes = 131072;
+
+// Byte offset that is out of range for every buffer descriptor we build, even
+// after the compiler folds an immediate offset (<= 4095) into it.
+constexpr uint32_t kOobOffset = 0xFFFFF000u;
+
 struct Pkt {
-    const uint8_t *base;  // 16-byte aligned chunk base
-    uint32_t nch;         // chunks covering the packet (0 for an empty packet)
+    uint64_t start;       // packet byte offset from the 16-byte aligned arena base
+    uint32_t nch;         // 16-byte chunks covering the packet (0 if empty)
     int s;                // first valid byte in chunk 0
     int e;                // bytes valid in the last chunk (1..16)
-    uint32_t w_hi;        // dot4 weights picking the BE-high bytes
+    bool big;             // > kNoWrapBytes: exact big-endian path
 };
 
 template <int G>
-__device__ __forceinline__ Pkt fetch_pkt(const CsumArgs &a, uint64_t d_start, uint32_t d_len, uint32_t src)
+__device__ __forceinline__ Pkt fetch_pkt(uint64_t d_start, uint32_t d_len, uint32_t src)
 {
     const uint32_t lo = bcast_from<G>(static_cast<uint32_t>(d_start), src);
     const uint32_t hi = bcast_from<G>(static_cast<uint32_t>(d_start >> 32), src);
     const uint32_t L = bcast_from<G>(d_len, src);
-    const uint64_t start = (static_cast<uint64_t>(hi) << 32) | lo;
     Pkt k;
-    k.s = static_cast<int>(start & 15);
-    k.base = a.arena + (start - static_cast<uint64_t>(k.s));
+    k.start = (static_cast<uint64_t>(hi) << 32) | lo;
+    k.s = static_cast<int>(k.start & 15);
     const uint64_t span = static_cast<uint64_t>(k.s) + L;
     k.nch = L ? static_cast<uint32_t>((span + 15) >> 4) : 0u;
     k.e = static_cast<int>(span - (static_cast<uint64_t>(k.nch ? k.nch - 1 : 0) << 4));
-    k.w_hi = (start & 1) ? 0x01000100u : 0x00010001u;
+    k.big = L > kNoWrapBytes;
     return k;
 }
 
-template <int G, int U, bool NT>
-__device__ __forceinline__ void issue_pass(const Pkt &k, uint32_t c0, uint4 (&v)[U])
+// Loads of one pass: chunk c = c0 + u*G of the packet, for u < U.  Branch-free:
+// a chunk past the packet's end reads zeros (buffer path: out-of-range offset;
+// global path: re-reads the packet's first chunk, then selects zero), so the
+// compiler can count outstanding loads exactly and keep the next round's
+// pass in flight while this one is consumed.
+template <int G, int U, bool NT, bool BUF>
+__device__ __forceinline__ void issue_pass(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, const Pkt &k, uint32_t c0,
+                                           uint4 (&v)[U])
 {
+    const uint64_t first = k.start - static_cast<uint64_t>(k.s);  // 16-aligned offset of chunk 0
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t c = c0 + u * G;
-        v[u] = (c < k.nch) ? load_chunk<NT>(k.base + (static_cast<uint64_t>(c) << 4)) : make_uint4(0, 0, 0, 0);
+        const bool in = c < k.nch;
+        if constexpr (BUF) {
+            const uint32_t off = in ? static_cast<uint32_t>(first + (static_cast<uint64_t>(c) << 4)) : kOobOffset;
+            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, NT ? 2 : 0);
+            v[u] = make_uint4(x.x, x.y, x.z, x.w);
+        } else {
+            const uint8_t *ptr = a.arena + first + (in ? (static_cast<uint64_t>(c) << 4) : 0);
+            const uint4 x = load_chunk<NT>(ptr);  // nch == 0 never reaches here (see caller)
+            v[u] = in ? x : make_uint4(0, 0, 0, 0);
+        }
     }
 }
 
 template <int G, int U>
-__device__ __forceinline__ void consume_pass(const Pkt &k, uint32_t c0, uint4 (&v)[U], uint32_t &hs, uint32_t &ls)
+__device__ __forceinline__ void mask_edges(const Pkt &k, uint32_t c0, uint4 (&v)[U])
 {
-    const uint32_t w_lo = k.w_hi ^ 0x01010101u;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t c = c0 + u * G;
@@ -270,28 +293,83 @@ __device__ __forceinline__ void consume_pass(const Pkt &k, uint32_t c0, uint4 (&
             v[u].z = keep_bytes(v[u].z, lo, hi, 8);
             v[u].w = keep_bytes(v[u].w, lo, hi, 12);
         }
-        hs = __builtin_amdgcn_udot4(v[u].x, k.w_hi, hs, false);
+    }
+}
+
+// Little-endian 16-bit word sum (v_sad_u16: lo16 + hi16 + acc, one op per dword).
+template <int U>
+__device__ __forceinline__ uint32_t sum_le(const uint4 (&v)[U], uint32_t acc)
+{
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        acc = __builtin_amdgcn_sad_u16(v[u].x, 0, acc);
+        acc = __builtin_amdgcn_sad_u16(v[u].y, 0, acc);
+        acc = __builtin_amdgcn_sad_u16(v[u].z, 0, acc);
+        acc = __builtin_amdgcn_sad_u16(v[u].w, 0, acc);
+    }
+    return acc;
+}
+
+// Exact big-endian word sum mod 2^32: 256 * (high-half bytes) + (low-half bytes).
+template <int U>
+__device__ __forceinline__ void sum_be(const uint4 (&v)[U], uint32_t w_hi, uint32_t &hs, uint32_t &ls)
+{
+    const uint32_t w_lo = w_hi ^ 0x01010101u;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        hs = __builtin_amdgcn_udot4(v[u].x, w_hi, hs, false);
         ls = __builtin_amdgcn_udot4(v[u].x, w_lo, ls, false);
-        hs = __builtin_amdgcn_udot4(v[u].y, k.w_hi, hs, false);
+        hs = __builtin_amdgcn_udot4(v[u].y, w_hi, hs, false);
         ls = __builtin_amdgcn_udot4(v[u].y, w_lo, ls, false);
-        hs = __builtin_amdgcn_udot4(v[u].z, k.w_hi, hs, false);
+        hs = __builtin_amdgcn_udot4(v[u].z, w_hi, hs, false);
         ls = __builtin_amdgcn_udot4(v[u].z, w_lo, ls, false);
-        hs = __builtin_amdgcn_udot4(v[u].w, k.w_hi, hs, false);
+        hs = __builtin_amdgcn_udot4(v[u].w, w_hi, hs, false);
         ls = __builtin_amdgcn_udot4(v[u].w, w_lo, ls, false);
     }
 }
 
-template <int G, int U, bool STRIDED, bool NT>
+// One packet's contribution from this lane.  `v` holds the (prefetched) first pass.
+template <int G, int U, bool NT, bool BUF>
+__device__ __forceinline__ uint32_t packet_partial(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, const Pkt &k,
+                                                   uint32_t sub, uint4 (&v)[U])
+{
+    constexpr uint32_t kPass = G * U;
+    mask_edges<G, U>(k, sub, v);
+    if (!k.big) {
+        uint32_t acc = sum_le<U>(v, 0u);
+        for (uint32_t c0 = kPass + sub; c0 < k.nch; c0 += kPass) {  // packets longer than one pass
+            uint4 x[U];
+            issue_pass<G, U, NT, BUF>(a, rsrc, k, c0, x);
+            mask_edges<G, U>(k, c0, x);
+            acc = sum_le<U>(x, acc);
+        }
+        return acc;  // LE-word sum, exact (< 2^32 for a packet of <= 128 KiB)
+    }
+    const uint32_t w_hi = (k.start & 1) ? 0x01000100u : 0x00010001u;
+    uint32_t hs = 0, ls = 0;
+    sum_be<U>(v, w_hi, hs, ls);
+    for (uint32_t c0 = kPass + sub; c0 < k.nch; c0 += kPass) {
+        uint4 x[U];
+        issue_pass<G, U, NT, BUF>(a, rsrc, k, c0, x);
+        mask_edges<G, U>(k, c0, x);
+        sum_be<U>(x, w_hi, hs, ls);
+    }
+    return (hs << 8) + ls;  // BE-word sum mod 2^32, exactly the reference's accumulator
+}
+
+template <int G, int U, bool STRIDED, bool NT, bool BUF>
 __global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
 {
     static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two in [4,64]");
-    constexpr uint32_t P = 64 / G;        // packets per round
-    constexpr uint32_t kPass = G * U;     // chunks per pass
+    constexpr uint32_t P = 64 / G;  // packets per round
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t sub = lane & (G - 1);
     const uint32_t grp = lane / G;
     const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
+    // Whole-arena buffer descriptor (used only when BUF: the arena fits a 32-bit offset).
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? a.arena_bytes : 0), 0x00020000);
 
     for (uint64_t base = static_cast<uint64_t>(wave) * 64; base < a.n; base += static_cast<uint64_t>(nwaves) * 64) {
         const uint64_t p = base + lane;
@@ -310,44 +388,53 @@ __global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
         }
         d_start += a.base_adjust;
         const bool d_ok = d_start <= a.arena_bytes && d_len <= a.arena_bytes - d_start;
-        if (!d_ok)
+        if (!d_ok || d_len == 0) {  // nothing to read; chunk 0 of offset 0 is a safe address
             d_len = 0;
+            d_start = 0;
+        }
 
-        uint32_t mine = 0;  // BE-word sum (mod 2^32) of this lane's packet
-        Pkt cur = fetch_pkt<G>(a, d_start, d_len, grp);
+        uint32_t mine = 0;  // this lane's packet: LE sum (<= 128 KiB) or BE sum (longer)
+        Pkt cur = fetch_pkt<G>(d_start, d_len, grp);
         uint4 v[U];
-        issue_pass<G, U, NT>(cur, sub, v);
+        issue_pass<G, U, NT, BUF>(a, rsrc, cur, sub, v);
         for (uint32_t r = 0; r < G; ++r) {
-            Pkt nxt = cur;
+            // Prefetch the next round's first pass.  Unconditional on purpose: on the
+            // last round it loads an empty packet (no memory traffic on the buffer
+            // path), so every path through the loop has the same loads outstanding
+            // and the compiler waits only for the pass it consumes (vmcnt(U)).
+            const bool has_next = r + 1 < G;
+            Pkt nxt = fetch_pkt<G>(d_start, d_len, (has_next ? r + 1 : r) * P + grp);
+            nxt.nch = has_next ? nxt.nch : 0u;
             uint4 w[U];
-            if (r + 1 < G) {  // prefetch the next round's first pass
-                nxt = fetch_pkt<G>(a, d_start, d_len, (r + 1) * P + grp);
-                issue_pass<G, U, NT>(nxt, sub, w);
-            }
-            uint32_t hs = 0, ls = 0;
-            consume_pass<G, U>(cur, sub, v, hs, ls);
-            for (uint32_t c0 = kPass + sub; c0 < cur.nch; c0 += kPass) {  // packets longer than one pass
-                uint4 x[U];
-                issue_pass<G, U, NT>(cur, c0, x);
-                consume_pass<G, U>(cur, c0, x, hs, ls);
-            }
-            const uint32_t words = group_allreduce<G>((hs << 8) + ls);
+            issue_pass<G, U, NT, BUF>(a, rsrc, nxt, sub, w);
+            const uint32_t words = group_allreduce<G>(packet_partial<G, U, NT, BUF>(a, rsrc, cur, sub, v));
             if constexpr (G == 64) {
                 mine = (lane == r) ? words : mine;
             } else {
                 const uint32_t t = bcast_from<G>(words, (lane % P) * G);  // group (lane % P)'s sum
                 mine = (lane / P == r) ? t : mine;
             }
-            if (r + 1 < G) {
-                cur = nxt;
+            cur = nxt;
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    v[u] = w[u];
-            }
+            for (int u = 0; u < U; ++u)
+                v[u] = w[u];
         }
-        uint32_t acc = d_seed + mine;  // util.rs:89-99 (mod 2^32)
-        while (acc > 0xffff)           // util.rs:101-103
-            acc = (acc & 0xffff) + (acc >> 16);
+        uint32_t acc;
+        if (d_len <= kNoWrapBytes) {
+            // seed + BE words, no wrap possible: equals seed + G where G is the LE
+            // sum folded and byte-swapped (a packet at an odd offset is already
+            // in BE order relative to the aligned words) — RFC 1071 §2(B).
+            uint32_t x = mine;
+            while (x > 0xffff)
+                x = (x & 0xffff) + (x >> 16);
+            const uint32_t g = (d_start & 1) ? x : (((x & 0xff) << 8) | (x >> 8));
+            acc = d_seed + g;
+            acc = (acc & 0xffff) + (acc >> 16);  // <= 0x1fffe: one end-around step folds it
+        } else {
+            acc = d_seed + mine;  // util.rs:89-99 (mod 2^32)
+            while (acc > 0xffff)  // util.rs:101-103
+                acc = (acc & 0xffff) + (acc >> 16);
+        }
         if (a.flags & RNS_FLAG_COMPLEMENT)
             acc ^= 0xffff;
         if (!d_ok)
@@ -399,11 +486,23 @@ int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipSt
     if (blocks == 0)
         return RNS_OK;
     const dim3 grid(static_cast<uint32_t>(blocks)), block(kBlock);
-    switch (variant) {
-    case 0: hipLaunchKernelGGL((csum_batch_kernel<G, U, S, false>), grid, block, 0, st, a); break;
-    case 1: hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, false>), grid, block, 0, st, a); break;
-    case 2: hipLaunchKernelGGL((csum_batch_kernel<G, U, S, true>), grid, block, 0, st, a); break;
-    default: hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true>), grid, block, 0, st, a); break;
+    const bool nt = (variant & 2) != 0;
+    if ((variant & 1) == 0) {
+        if (nt)
+            hipLaunchKernelGGL((csum_batch_kernel<G, U, S, true>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_batch_kernel<G, U, S, false>), grid, block, 0, st, a);
+    } else {
+        // Buffer loads need the arena inside one 32-bit offset range (kOobOffset stays out of it).
+        const bool buf = a.arena_bytes < kOobOffset;
+        if (nt && buf)
+            hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, true>), grid, block, 0, st, a);
+        else if (nt)
+            hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, false>), grid, block, 0, st, a);
+        else if (buf)
+            hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, false, true>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, false, false>), grid, block, 0, st, a);
     }
     return hip_status(hipGetLastError());
 }

@@ -25,8 +25,9 @@ def main():
     if args.shapes:
         shapes = [tuple(int(x) for x in s.split(",")) for s in args.shapes.split(";")]
     else:
-        shapes = [(v, g, u, 0) for v in (0, 2) for g in (8, 16, 32, 64) for u in (2, 4)]
-        shapes += [(v, g, u, mb) for v in (1, 3) for g in (4, 8, 16, 32, 64) for u in (1, 2, 4) for mb in (0, 2048)]
+        shapes = [(v, g, u, 0) for v in (0, 2) for g in (16, 64) for u in (2, 4)]
+        shapes += [(v, g, u, 0) for v in (1, 3) for g in (4, 8, 16, 32, 64) for u in (1, 2, 4, 8)]
+        shapes += [(v, 4, u, 2048) for v in (1, 3) for u in (1, 2)]
     results = {}
     for cfg in args.configs.split(","):
         lay = make_layout(cfg)
