@@ -118,7 +118,8 @@ int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uin
 /* Tuning entry (bench / tests): explicit kernel shape.  variant bit 0: 0 = group
  * kernel (one lane stores each result), 1 = rounds kernel (a wave owns 64
  * consecutive packets, one coalesced result store); bit 1: nontemporal packet
- * loads.  lanes_per_packet in
+ * loads; bit 2: mixed kernel (rounds kernel that sorts each wave's 64 packets
+ * into size classes, each with its own shape; G and U are ignored).  lanes_per_packet in
  * {4,8,16,32,64}; unroll (16-byte chunks in flight per lane per pass) in
  * {1,2,4,8}; max_blocks = grid cap (0 = no grid-stride loop). */
 int rns_csum_batch_dev_cfg(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off,

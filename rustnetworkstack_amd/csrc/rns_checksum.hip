@@ -337,11 +337,10 @@ __device__ __forceinline__ uint32_t packet_partial(const CsumArgs &a, __amdgpu_b
     mask_edges<G, U>(k, sub, v);
     if (!k.big) {
         uint32_t acc = sum_le<U>(v, 0u);
-        for (uint32_t c0 = kPass + sub; c0 < k.nch; c0 += kPass) {  // packets longer than one pass
-            uint4 x[U];
-            issue_pass<G, U, NT, BUF>(a, rsrc, k, c0, x);
-            mask_edges<G, U>(k, c0, x);
-            acc = sum_le<U>(x, acc);
+        for (uint32_t c0 = kPass + sub; c0 < k.nch; c0 += kPass) {  // packets longer than one pass (reuse v)
+            issue_pass<G, U, NT, BUF>(a, rsrc, k, c0, v);
+            mask_edges<G, U>(k, c0, v);
+            acc = sum_le<U>(v, acc);
         }
         return acc;  // LE-word sum, exact (< 2^32 for a packet of <= 128 KiB)
     }
@@ -349,12 +348,36 @@ __device__ __forceinline__ uint32_t packet_partial(const CsumArgs &a, __amdgpu_b
     uint32_t hs = 0, ls = 0;
     sum_be<U>(v, w_hi, hs, ls);
     for (uint32_t c0 = kPass + sub; c0 < k.nch; c0 += kPass) {
-        uint4 x[U];
-        issue_pass<G, U, NT, BUF>(a, rsrc, k, c0, x);
-        mask_edges<G, U>(k, c0, x);
-        sum_be<U>(x, w_hi, hs, ls);
+        issue_pass<G, U, NT, BUF>(a, rsrc, k, c0, v);
+        mask_edges<G, U>(k, c0, v);
+        sum_be<U>(v, w_hi, hs, ls);
     }
     return (hs << 8) + ls;  // BE-word sum mod 2^32, exactly the reference's accumulator
+}
+
+// Owner-lane finish: seed + this packet's word sum -> the reference's folded u16.
+__device__ __forceinline__ uint16_t finalize(uint32_t mine, uint64_t d_start, uint32_t d_len, uint32_t d_seed,
+                                             bool d_ok, uint32_t flags)
+{
+    uint32_t acc;
+    if (d_len <= kNoWrapBytes) {
+        // seed + BE words, no wrap possible: equals seed + G where G is the LE
+        // sum folded and byte-swapped (a packet at an odd offset is already in
+        // BE order relative to the aligned words) — RFC 1071 §2(B).
+        uint32_t x = mine;
+        while (x > 0xffff)
+            x = (x & 0xffff) + (x >> 16);
+        const uint32_t g = (d_start & 1) ? x : (((x & 0xff) << 8) | (x >> 8));
+        acc = d_seed + g;
+        acc = (acc & 0xffff) + (acc >> 16);  // <= 0x1fffe: one end-around step folds it
+    } else {
+        acc = d_seed + mine;  // util.rs:89-99 (mod 2^32)
+        while (acc > 0xffff)  // util.rs:101-103
+            acc = (acc & 0xffff) + (acc >> 16);
+    }
+    if (flags & RNS_FLAG_COMPLEMENT)
+        acc ^= 0xffff;
+    return d_ok ? static_cast<uint16_t>(acc) : static_cast<uint16_t>(0);
 }
 
 template <int G, int U, bool STRIDED, bool NT, bool BUF>
@@ -419,28 +442,145 @@ __global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
             for (int u = 0; u < U; ++u)
                 v[u] = w[u];
         }
-        uint32_t acc;
-        if (d_len <= kNoWrapBytes) {
-            // seed + BE words, no wrap possible: equals seed + G where G is the LE
-            // sum folded and byte-swapped (a packet at an odd offset is already
-            // in BE order relative to the aligned words) — RFC 1071 §2(B).
-            uint32_t x = mine;
-            while (x > 0xffff)
-                x = (x & 0xffff) + (x >> 16);
-            const uint32_t g = (d_start & 1) ? x : (((x & 0xff) << 8) | (x >> 8));
-            acc = d_seed + g;
-            acc = (acc & 0xffff) + (acc >> 16);  // <= 0x1fffe: one end-around step folds it
-        } else {
-            acc = d_seed + mine;  // util.rs:89-99 (mod 2^32)
-            while (acc > 0xffff)  // util.rs:101-103
-                acc = (acc & 0xffff) + (acc >> 16);
-        }
-        if (a.flags & RNS_FLAG_COMPLEMENT)
-            acc ^= 0xffff;
-        if (!d_ok)
-            acc = 0;
+        const uint16_t acc = finalize(mine, d_start, d_len, d_seed, d_ok, a.flags);
         if (live)
             a.out[p] = static_cast<uint16_t>(acc);  // 64 consecutive u16: one 128-byte store
+        if (a.bad) {
+            const uint64_t rejected = __ballot(live && !d_ok);
+            if (rejected && lane == 0)
+                atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// v3: "mixed" kernel — the rounds kernel for batches whose packet sizes vary
+// (IMIX).  A wavefront still owns 64 consecutive packets, but first SORTS them
+// by size class inside the wave (ballot + mbcnt ranks, one ds_permute per
+// descriptor word), then runs each class with its own lanes-per-packet shape,
+// so a 40 B packet never holds 16 lanes idle while a 1500 B packet finishes.
+// Results return to the owner lane (its class, round and group are known from
+// its rank) and leave in one 128-byte store, as in v2.
+// ---------------------------------------------------------------------------
+struct ClassRun {
+    uint32_t off;   // first sorted position of the class (wave-uniform)
+    uint32_t cnt;   // packets in the class (wave-uniform)
+};
+
+template <int G, int U, bool NT, bool BUF>
+__device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, ClassRun cr,
+                                          uint64_t s_start, uint32_t s_len, bool in_class, uint32_t rank,
+                                          uint32_t lane, uint32_t &mine)
+{
+    constexpr uint32_t P = 64 / G;
+    const uint32_t sub = lane & (G - 1);
+    const uint32_t grp = lane / G;
+    const uint32_t rounds = (cr.cnt + P - 1) / P;
+    if (rounds == 0)
+        return;
+    // group `grp` of round r takes sorted position off + r*P + grp (if inside the class)
+    auto fetch = [&](uint32_t r) {
+        const uint32_t i = r * P + grp;
+        Pkt k = fetch_pkt<G>(s_start, s_len, cr.off + (i < cr.cnt ? i : 0));
+        k.nch = (i < cr.cnt) ? k.nch : 0u;
+        return k;
+    };
+    Pkt cur = fetch(0);
+    uint4 v[U];
+    issue_pass<G, U, NT, BUF>(a, rsrc, cur, sub, v);
+    for (uint32_t r = 0; r < rounds; ++r) {
+        const bool has_next = r + 1 < rounds;
+        Pkt nxt = fetch(has_next ? r + 1 : r);
+        nxt.nch = has_next ? nxt.nch : 0u;
+        uint4 w[U];
+        issue_pass<G, U, NT, BUF>(a, rsrc, nxt, sub, w);  // prefetch: see csum_rounds_kernel
+        const uint32_t words = group_allreduce<G>(packet_partial<G, U, NT, BUF>(a, rsrc, cur, sub, v));
+        if constexpr (G == 64) {
+            const uint32_t t = words;  // wave-uniform
+            mine = (in_class && rank == r) ? t : mine;
+        } else {
+            const uint32_t t = bcast_from<G>(words, (rank % P) * G);
+            mine = (in_class && rank / P == r) ? t : mine;
+        }
+        cur = nxt;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            v[u] = w[u];
+    }
+}
+
+// Size classes (in 16-byte chunks a packet spans) and the shape each runs with.
+constexpr uint32_t kClassMax[4] = {8, 32, 64, 128};  // tiny, small, medium, large; above: jumbo
+
+template <bool STRIDED, bool NT, bool BUF>
+__global__ __launch_bounds__(kBlock) void csum_mixed_kernel(const CsumArgs a)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? a.arena_bytes : 0), 0x00020000);
+
+    for (uint64_t base = static_cast<uint64_t>(wave) * 64; base < a.n; base += static_cast<uint64_t>(nwaves) * 64) {
+        const uint64_t p = base + lane;
+        const bool live = p < a.n;
+        uint64_t d_start = 0;
+        uint32_t d_len = 0, d_seed = 0;
+        if (live) {
+            if constexpr (STRIDED) {
+                d_start = a.first_off + p * a.stride;
+                d_len = a.fixed_len;
+            } else {
+                d_start = a.off[p];
+                d_len = a.len[p];
+            }
+            d_seed = a.seed ? a.seed[p] : 0u;
+        }
+        d_start += a.base_adjust;
+        const bool d_ok = d_start <= a.arena_bytes && d_len <= a.arena_bytes - d_start;
+        if (!d_ok || d_len == 0) {
+            d_len = 0;
+            d_start = 0;
+        }
+        // size class of this lane's packet
+        const uint32_t nch = d_len ? static_cast<uint32_t>(((d_start & 15) + d_len + 15) >> 4) : 0u;
+        const uint32_t cls = (nch <= kClassMax[0]) ? 0u : (nch <= kClassMax[1]) ? 1u
+                           : (nch <= kClassMax[2]) ? 2u : (nch <= kClassMax[3]) ? 3u : 4u;
+        uint32_t pos = 0, rank = 0;
+        ClassRun cr[5];
+        uint32_t off = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < 5; ++c) {
+            const uint64_t m = __ballot(cls == c);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+            if (cls == c) {
+                rank = below;
+                pos = off + below;
+            }
+            cr[c] = ClassRun{off, static_cast<uint32_t>(__popcll(m))};
+            off += cr[c].cnt;
+        }
+        // sort the descriptors by class: lane `pos` receives this lane's packet
+        const uint32_t addr = pos * 4;
+        const uint32_t s_lo = static_cast<uint32_t>(
+            __builtin_amdgcn_ds_permute(static_cast<int>(addr), static_cast<int>(static_cast<uint32_t>(d_start))));
+        const uint32_t s_hi = static_cast<uint32_t>(
+            __builtin_amdgcn_ds_permute(static_cast<int>(addr), static_cast<int>(static_cast<uint32_t>(d_start >> 32))));
+        const uint32_t s_len = static_cast<uint32_t>(
+            __builtin_amdgcn_ds_permute(static_cast<int>(addr), static_cast<int>(d_len)));
+        const uint64_t s_start = (static_cast<uint64_t>(s_hi) << 32) | s_lo;
+
+        uint32_t mine = 0;
+        run_class<4, 2, NT, BUF>(a, rsrc, cr[0], s_start, s_len, cls == 0, rank, lane, mine);
+        run_class<8, 4, NT, BUF>(a, rsrc, cr[1], s_start, s_len, cls == 1, rank, lane, mine);
+        run_class<16, 4, NT, BUF>(a, rsrc, cr[2], s_start, s_len, cls == 2, rank, lane, mine);
+        run_class<32, 4, NT, BUF>(a, rsrc, cr[3], s_start, s_len, cls == 3, rank, lane, mine);
+        run_class<64, 4, NT, BUF>(a, rsrc, cr[4], s_start, s_len, cls == 4, rank, lane, mine);
+
+        const uint16_t res = finalize(mine, d_start, d_len, d_seed, d_ok, a.flags);
+        if (live)
+            a.out[p] = res;  // 64 consecutive u16: one 128-byte store
         if (a.bad) {
             const uint64_t rejected = __ballot(live && !d_ok);
             if (rejected && lane == 0)
@@ -474,7 +614,7 @@ template <int G, int U, bool S>
 int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipStream_t st)
 {
     uint64_t blocks;
-    if ((variant & 1) == 0) {
+    if ((variant & 5) == 0) {
         constexpr uint32_t kGroups = kBlock / G;
         blocks = (static_cast<uint64_t>(a.n) + kGroups - 1) / kGroups;
     } else {
@@ -487,14 +627,22 @@ int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipSt
         return RNS_OK;
     const dim3 grid(static_cast<uint32_t>(blocks)), block(kBlock);
     const bool nt = (variant & 2) != 0;
-    if ((variant & 1) == 0) {
+    const bool buf = a.arena_bytes < kOobOffset;  // buffer loads need a 32-bit offset range
+    if (variant & 4) {
+        if (nt && buf)
+            hipLaunchKernelGGL((csum_mixed_kernel<S, true, true>), grid, block, 0, st, a);
+        else if (nt)
+            hipLaunchKernelGGL((csum_mixed_kernel<S, true, false>), grid, block, 0, st, a);
+        else if (buf)
+            hipLaunchKernelGGL((csum_mixed_kernel<S, false, true>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_mixed_kernel<S, false, false>), grid, block, 0, st, a);
+    } else if ((variant & 1) == 0) {
         if (nt)
             hipLaunchKernelGGL((csum_batch_kernel<G, U, S, true>), grid, block, 0, st, a);
         else
             hipLaunchKernelGGL((csum_batch_kernel<G, U, S, false>), grid, block, 0, st, a);
     } else {
-        // Buffer loads need the arena inside one 32-bit offset range (kOobOffset stays out of it).
-        const bool buf = a.arena_bytes < kOobOffset;
         if (nt && buf)
             hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, true>), grid, block, 0, st, a);
         else if (nt)
@@ -510,8 +658,10 @@ int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipSt
 template <bool S>
 int dispatch(const CsumArgs &a, uint32_t variant, uint32_t G, uint32_t U, uint32_t max_blocks, hipStream_t st)
 {
-    if (variant > 3)
+    if (variant > 7)
         return RNS_E_INVALID;
+    if (variant & 4)  // the mixed kernel picks its own per-class shapes
+        return launch_shape<64, 4, S>(a, variant, max_blocks, st);
 #define RNS_SHAPE(g, u) \
     if (G == g && U == u) return launch_shape<g, u, S>(a, variant, max_blocks, st);
     RNS_SHAPE(4, 1) RNS_SHAPE(4, 2) RNS_SHAPE(4, 4) RNS_SHAPE(4, 8)
@@ -848,11 +998,12 @@ int rns_fill_splitmix64_dev(uint8_t *d_buf, uint64_t nbytes, uint64_t seed, void
 
 const char *rns_csum_shape_name(uint32_t len_hint)
 {
-    static const char *const names[] = {"csum_batch_kernel", "csum_rounds_kernel", "csum_batch_kernel[nt]",
-                                        "csum_rounds_kernel[nt]"};
+    static const char *const names[] = {"csum_batch_kernel",     "csum_rounds_kernel",     "csum_batch_kernel[nt]",
+                                        "csum_rounds_kernel[nt]", "csum_mixed_kernel",      "csum_mixed_kernel",
+                                        "csum_mixed_kernel[nt]",  "csum_mixed_kernel[nt]"};
     static thread_local char buf[96];
     const Shape sh = pick_shape(len_hint);
-    std::snprintf(buf, sizeof(buf), "%s<G=%u,U=%u>%s", names[sh.variant & 3], sh.G, sh.U,
+    std::snprintf(buf, sizeof(buf), "%s<G=%u,U=%u>%s", names[sh.variant & 7], sh.G, sh.U,
                   sh.max_blocks ? " grid-capped" : "");
     return buf;
 }

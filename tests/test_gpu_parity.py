@@ -20,6 +20,7 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
 SHAPES = [(var, g, u) for var in (0, 1) for g in (4, 8, 16, 32, 64) for u in (1, 2, 4, 8)]
+SHAPES += [(var, 64, 4) for var in (2, 3, 4, 6)]
 
 
 def host_u16(t: torch.Tensor) -> np.ndarray:
@@ -85,7 +86,7 @@ def test_length_by_alignment_sweep(oracle):
     arena = torch.from_numpy(arena_np).to(DEV)
     d_off, d_len, d_sd = dev_desc(off, lens, sd)
     for shape in (None, (0, 4, 1, 0), (0, 64, 2, 512), (1, 4, 1, 0), (1, 16, 2, 0), (1, 64, 4, 0), (1, 8, 8, 3),
-                  (1, 64, 2, 512)):
+                  (1, 64, 2, 512), (3, 16, 8, 0), (4, 0, 0, 0), (6, 0, 0, 0), (6, 0, 0, 7)):
         out = csum_batch(arena, d_off, d_len, d_sd, complement=True, shape=shape, len_hint=1024)
         assert np.array_equal(host_u16(out), expect), shape
 
@@ -107,7 +108,8 @@ def test_edge_patterns_and_zero_handling(oracle):
     expect = oracle.batch(arena_np, off, ln, sd)
     arena = torch.from_numpy(arena_np).to(DEV)
     d = dev_desc(off, ln, sd)
-    for shape in (None, (0, 4, 4, 0), (0, 64, 1, 0), (1, 4, 4, 0), (1, 32, 8, 0), (1, 64, 1, 5)):
+    for shape in (None, (0, 4, 4, 0), (0, 64, 1, 0), (1, 4, 4, 0), (1, 32, 8, 0), (1, 64, 1, 5), (4, 0, 0, 0),
+                  (6, 0, 0, 3)):
         assert np.array_equal(host_u16(csum_batch(arena, *d, shape=shape)), expect), shape
     # all-zero payload with seed 0 is 0 (checksum 0xffff); an even run of 0xff folds to 0xffff (checksum 0)
     assert expect[rows.index((0, 1500, 0))] == 0
@@ -144,8 +146,9 @@ def test_unaligned_arena_base(oracle):
         ln = (O.splitmix64_words(shift, n) % np.uint64(1600) + np.uint64(1)).astype(np.uint32)
         off = (O.splitmix64_words(shift + 100, n) % np.uint64((1 << 20) - 2000)).astype(np.uint64)
         expect = oracle.batch(host[shift:], off, ln, None, complement=True)
-        out = csum_batch(view, *dev_desc(off, ln, None), complement=True)
-        assert np.array_equal(host_u16(out), expect), shift
+        for shape in (None, (4, 0, 0, 0), (3, 16, 8, 0)):
+            out = csum_batch(view, *dev_desc(off, ln, None), complement=True, shape=shape)
+            assert np.array_equal(host_u16(out), expect), (shift, shape)
 
 
 def test_strided_api(oracle):

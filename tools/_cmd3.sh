@@ -1,5 +1,5 @@
 set -u
-cd $GRAFT_REPO_ROOT; O=gpurun_out/r01c; mkdir -p $O; export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT; O=gpurun_out/r01g; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $O/pytest_gpu.log 2>&1; rc=$?; echo pytest rc=$rc; tail -5 $O/pytest_gpu.log
 case $rc in 124|134|137|139) exit $rc;; esac
 timeout -k 10 120 ./tools/hbm_read_probe > $O/probe.log 2>&1; rc=$?; echo probe rc=$rc

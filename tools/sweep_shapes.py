@@ -28,6 +28,7 @@ def main():
         shapes = [(v, g, u, 0) for v in (0, 2) for g in (16, 64) for u in (2, 4)]
         shapes += [(v, g, u, 0) for v in (1, 3) for g in (4, 8, 16, 32, 64) for u in (1, 2, 4, 8)]
         shapes += [(v, 4, u, 2048) for v in (1, 3) for u in (1, 2)]
+        shapes += [(v, 0, 0, mb) for v in (4, 6) for mb in (0, 1024, 2048, 4096)]
     results = {}
     for cfg in args.configs.split(","):
         lay = make_layout(cfg)
