@@ -214,7 +214,9 @@ __device__ __forceinline__ uint32_t group_allreduce(uint32_t v)
 template <int G>
 __device__ __forceinline__ uint32_t bcast_from(uint32_t v, uint32_t src)
 {
-    if constexpr (G == 64)
+    if constexpr (G == 1)
+        return v;  // one lane per packet: used only for the first class (offset 0, one round), where src == lane
+    else if constexpr (G == 64)
         return __builtin_amdgcn_readlane(v, src);  // src is wave-uniform
     else
         return static_cast<uint32_t>(__shfl(static_cast<int>(v), static_cast<int>(src), 64));
@@ -476,6 +478,8 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
     const uint32_t sub = lane & (G - 1);
     const uint32_t grp = lane / G;
     const uint32_t rounds = (cr.cnt + P - 1) / P;
+    // G == 1 reads each lane's own sorted descriptor (bcast_from<1>), valid because the
+    // one-lane class is class 0: offset 0 and at most 64 packets, so position == lane.
     if (rounds == 0)
         return;
     // group `grp` of round r takes sorted position off + r*P + grp (if inside the class)
@@ -499,7 +503,7 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
             const uint32_t t = words;  // wave-uniform
             mine = (in_class && rank == r) ? t : mine;
         } else {
-            const uint32_t t = bcast_from<G>(words, (rank % P) * G);
+            const uint32_t t = static_cast<uint32_t>(__shfl(static_cast<int>(words), static_cast<int>((rank % P) * G), 64));
             mine = (in_class && rank / P == r) ? t : mine;
         }
         cur = nxt;
@@ -510,7 +514,7 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
 }
 
 // Size classes (in 16-byte chunks a packet spans) and the shape each runs with.
-constexpr uint32_t kClassMax[4] = {8, 32, 64, 128};  // tiny, small, medium, large; above: jumbo
+constexpr uint32_t kClassMax[4] = {4, 16, 64, 128};  // tiny, small, medium, large; above: jumbo
 
 template <bool STRIDED, bool NT, bool BUF>
 __global__ __launch_bounds__(kBlock) void csum_mixed_kernel(const CsumArgs a)
@@ -572,8 +576,8 @@ __global__ __launch_bounds__(kBlock) void csum_mixed_kernel(const CsumArgs a)
         const uint64_t s_start = (static_cast<uint64_t>(s_hi) << 32) | s_lo;
 
         uint32_t mine = 0;
-        run_class<4, 2, NT, BUF>(a, rsrc, cr[0], s_start, s_len, cls == 0, rank, lane, mine);
-        run_class<8, 4, NT, BUF>(a, rsrc, cr[1], s_start, s_len, cls == 1, rank, lane, mine);
+        run_class<1, 4, NT, BUF>(a, rsrc, cr[0], s_start, s_len, cls == 0, rank, lane, mine);
+        run_class<4, 4, NT, BUF>(a, rsrc, cr[1], s_start, s_len, cls == 1, rank, lane, mine);
         run_class<16, 4, NT, BUF>(a, rsrc, cr[2], s_start, s_len, cls == 2, rank, lane, mine);
         run_class<32, 4, NT, BUF>(a, rsrc, cr[3], s_start, s_len, cls == 3, rank, lane, mine);
         run_class<64, 4, NT, BUF>(a, rsrc, cr[4], s_start, s_len, cls == 4, rank, lane, mine);

@@ -32,6 +32,11 @@ CONFIGS = {
     "c5_imix": dict(n=1 << 23, kind="imix"),
 }
 HEADLINE = "c3_1500B"
+# Diagnostic batches (not BASELINE.json configs): one IMIX size each, for per-class tuning.
+DIAG_CONFIGS = {
+    "d40B": dict(n=1 << 22, kind="fixed", length=40),
+    "d576B": dict(n=1 << 21, kind="fixed", length=576),
+}
 IMIX_SIZES = (40, 576, 1500)  # 7:4:1
 
 
@@ -81,7 +86,7 @@ def make_layout(name: str, n: int | None = None, data_seed: int = DATA_SEED, sha
                 align: int = ALIGN) -> Layout:
     """Packets of config `name`; `shard=(rank, world)` keeps the contiguous
     packet-index range ceil(n/world) of that rank."""
-    cfg = CONFIGS[name]
+    cfg = CONFIGS[name] if name in CONFIGS else DIAG_CONFIGS[name]
     total = cfg["n"] if n is None else n
     if cfg["kind"] == "fixed":
         length_all = None

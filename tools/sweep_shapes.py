@@ -17,7 +17,7 @@ from rustnetworkstack_amd.workloads import DeviceBatch, make_layout  # noqa: E40
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="c3_1500B,c4_9000B,c2_64B,c5_imix")
+    ap.add_argument("--configs", default="c3_1500B,c4_9000B,c2_64B,c5_imix,d40B,d576B")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--shapes", default="")
