@@ -214,9 +214,7 @@ __device__ __forceinline__ uint32_t group_allreduce(uint32_t v)
 template <int G>
 __device__ __forceinline__ uint32_t bcast_from(uint32_t v, uint32_t src)
 {
-    if constexpr (G == 1)
-        return v;  // one lane per packet: used only for the first class (offset 0, one round), where src == lane
-    else if constexpr (G == 64)
+    if constexpr (G == 64)
         return __builtin_amdgcn_readlane(v, src);  // src is wave-uniform
     else
         return static_cast<uint32_t>(__shfl(static_cast<int>(v), static_cast<int>(src), 64));
@@ -478,8 +476,6 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
     const uint32_t sub = lane & (G - 1);
     const uint32_t grp = lane / G;
     const uint32_t rounds = (cr.cnt + P - 1) / P;
-    // G == 1 reads each lane's own sorted descriptor (bcast_from<1>), valid because the
-    // one-lane class is class 0: offset 0 and at most 64 packets, so position == lane.
     if (rounds == 0)
         return;
     // group `grp` of round r takes sorted position off + r*P + grp (if inside the class)
@@ -576,7 +572,7 @@ __global__ __launch_bounds__(kBlock) void csum_mixed_kernel(const CsumArgs a)
         const uint64_t s_start = (static_cast<uint64_t>(s_hi) << 32) | s_lo;
 
         uint32_t mine = 0;
-        run_class<1, 4, NT, BUF>(a, rsrc, cr[0], s_start, s_len, cls == 0, rank, lane, mine);
+        run_class<4, 1, NT, BUF>(a, rsrc, cr[0], s_start, s_len, cls == 0, rank, lane, mine);
         run_class<4, 4, NT, BUF>(a, rsrc, cr[1], s_start, s_len, cls == 1, rank, lane, mine);
         run_class<16, 4, NT, BUF>(a, rsrc, cr[2], s_start, s_len, cls == 2, rank, lane, mine);
         run_class<32, 4, NT, BUF>(a, rsrc, cr[3], s_start, s_len, cls == 3, rank, lane, mine);
@@ -677,13 +673,14 @@ int dispatch(const CsumArgs &a, uint32_t variant, uint32_t G, uint32_t U, uint32
     return RNS_E_INVALID;
 }
 
-// Kernel shape for a typical packet length (chunks of 16 B a packet spans),
-// from the interleaved shape sweep on MI355X (tools/sweep_shapes.py,
-// profiles/r01_sweep.json):
-//   <= 8 chunks  (64 B)    rounds, nontemporal, G=4,  U=1, grid 2048  (c2)
-//   <= 48 chunks (IMIX)    rounds,              G=4,  U=4             (c5: mixed 40/576/1500 B)
-//   <= 160 chunks (1500 B) rounds, nontemporal, G=32, U=4             (c3, headline)
-//   longer (9000 B)        group,  nontemporal, G=64, U=4             (c4)
+// Kernel shape for a typical (mean) packet length, in 16-byte chunks, from the
+// interleaved shape sweeps on MI355X (tools/sweep_shapes.py, profiles/r01_sweep*.json):
+//   <= 8 chunks   (64 B)        rounds, nontemporal, G=4, U=1, grid 2048      (c2)
+//   <= 48 chunks  (IMIX mean)   mixed (per-wave size-class sort)              (c5)
+//   <= 160 chunks (1500 B)      mixed, nontemporal (= rounds G=32,U=4 here)   (c3, headline)
+//   longer        (9000 B)      group, nontemporal, G=64, U=4                 (c4)
+// The mixed kernel is the robust choice for any size distribution; the other
+// two win by a few percent on batches of uniformly tiny / jumbo packets.
 struct Shape {
     uint32_t variant, G, U, max_blocks;
 };
@@ -694,9 +691,9 @@ Shape pick_shape(uint32_t len_hint)
     if (chunks <= 8)
         return Shape{3u, 4u, 1u, 2048u};
     if (chunks <= 48)
-        return Shape{1u, 4u, 4u, 0u};
+        return Shape{4u, 0u, 0u, 0u};
     if (chunks <= 160)
-        return Shape{3u, 32u, 4u, 0u};
+        return Shape{6u, 0u, 0u, 0u};
     return Shape{2u, 64u, 4u, 0u};
 }
 
@@ -1007,8 +1004,11 @@ const char *rns_csum_shape_name(uint32_t len_hint)
                                         "csum_mixed_kernel[nt]",  "csum_mixed_kernel[nt]"};
     static thread_local char buf[96];
     const Shape sh = pick_shape(len_hint);
-    std::snprintf(buf, sizeof(buf), "%s<G=%u,U=%u>%s", names[sh.variant & 7], sh.G, sh.U,
-                  sh.max_blocks ? " grid-capped" : "");
+    if (sh.variant & 4)
+        std::snprintf(buf, sizeof(buf), "%s (size classes G/U 4/1, 4/4, 16/4, 32/4, 64/4)", names[sh.variant & 7]);
+    else
+        std::snprintf(buf, sizeof(buf), "%s<G=%u,U=%u>%s", names[sh.variant & 7], sh.G, sh.U,
+                      sh.max_blocks ? " grid-capped" : "");
     return buf;
 }
 
