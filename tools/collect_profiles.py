@@ -1,0 +1,57 @@
+"""Copy the judged evidence of one gpurun session (gpurun_out/<tag>/) into profiles/.
+
+    python tools/collect_profiles.py r01i --round r01
+
+Writes profiles/<round>_bench_<config>.json (the bench JSON lines),
+profiles/<round>_rocprof_kernel_stats.csv / _kernel_trace.csv (rocprofv3
+--kernel-trace --stats of `bench.py`), profiles/traffic_<config>.json (PMC
+FETCH_SIZE/WRITE_SIZE per launch, read by bench.py) and the sweep JSON if present.
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--round", default="r01")
+    args = ap.parse_args()
+    src = os.path.join(ROOT, "gpurun_out", args.tag)
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    for name in sorted(os.listdir(src)):
+        if name.startswith("bench") and name.endswith(".log"):
+            lines = [ln for ln in open(os.path.join(src, name)) if ln.startswith("{")]
+            if lines:
+                d = json.loads(lines[-1])
+                cfg = d["config"]["workload"].split(":")[0]
+                with open(os.path.join(dst, f"{args.round}_bench_{cfg}.json"), "w") as f:
+                    json.dump(d, f, indent=1)
+    prof = os.path.join(src, "prof")
+    for kind in ("kernel_stats", "kernel_trace"):
+        p = os.path.join(prof, f"run_{kind}.csv")
+        if os.path.exists(p):
+            shutil.copy(p, os.path.join(dst, f"{args.round}_rocprof_c3_1500B_{kind}.csv"))
+    for name in os.listdir(src):
+        if name.startswith("traffic_") and name.endswith(".json"):
+            d = json.load(open(os.path.join(src, name)))
+            d["source"] = d["source"].replace(src, f"gpurun_out/{args.tag}").split("/repo/")[-1]
+            d["collected"] = f"{args.round} gpurun session {args.tag}"
+            with open(os.path.join(dst, name), "w") as f:
+                json.dump(d, f, indent=1)
+    sw = os.path.join(src, "sweep.log")
+    if os.path.exists(sw):
+        lines = [ln for ln in open(sw) if ln.startswith("{")]
+        if lines:
+            with open(os.path.join(dst, f"{args.round}_sweep_{args.tag}.json"), "w") as f:
+                json.dump(json.loads(lines[-1]), f, indent=1)
+    print(sorted(os.listdir(dst)))
+
+
+if __name__ == "__main__":
+    sys.exit(main())
