@@ -40,7 +40,8 @@ def main():
     for name in os.listdir(src):
         if name.startswith("traffic_") and name.endswith(".json"):
             d = json.load(open(os.path.join(src, name)))
-            d["source"] = d["source"].replace(src, f"gpurun_out/{args.tag}").split("/repo/")[-1]
+            d["source"] = (f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes over "
+                           f"`bench.py --steps 5 --warmup 1` (gpurun_out/{args.tag}/pmc_fetch, pmc_write)")
             d["collected"] = f"{args.round} gpurun session {args.tag}"
             with open(os.path.join(dst, name), "w") as f:
                 json.dump(d, f, indent=1)
