@@ -237,14 +237,10 @@ struct Pkt {
     bool big;             // > kNoWrapBytes: exact big-endian path
 };
 
-template <int G>
-__device__ __forceinline__ Pkt fetch_pkt(uint64_t d_start, uint32_t d_len, uint32_t src)
+__device__ __forceinline__ Pkt make_pkt(uint64_t start, uint32_t L)
 {
-    const uint32_t lo = bcast_from<G>(static_cast<uint32_t>(d_start), src);
-    const uint32_t hi = bcast_from<G>(static_cast<uint32_t>(d_start >> 32), src);
-    const uint32_t L = bcast_from<G>(d_len, src);
     Pkt k;
-    k.start = (static_cast<uint64_t>(hi) << 32) | lo;
+    k.start = start;
     k.s = static_cast<int>(k.start & 15);
     const uint64_t span = static_cast<uint64_t>(k.s) + L;
     k.nch = L ? static_cast<uint32_t>((span + 15) >> 4) : 0u;
@@ -253,14 +249,23 @@ __device__ __forceinline__ Pkt fetch_pkt(uint64_t d_start, uint32_t d_len, uint3
     return k;
 }
 
+template <int G>
+__device__ __forceinline__ Pkt fetch_pkt(uint64_t d_start, uint32_t d_len, uint32_t src)
+{
+    const uint32_t lo = bcast_from<G>(static_cast<uint32_t>(d_start), src);
+    const uint32_t hi = bcast_from<G>(static_cast<uint32_t>(d_start >> 32), src);
+    const uint32_t L = bcast_from<G>(d_len, src);
+    return make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L);
+}
+
 // Loads of one pass: chunk c = c0 + u*G of the packet, for u < U.  Branch-free:
 // a chunk past the packet's end reads zeros (buffer path: out-of-range offset;
 // global path: re-reads the packet's first chunk, then selects zero), so the
 // compiler can count outstanding loads exactly and keep the next round's
 // pass in flight while this one is consumed.
-template <int G, int U, bool NT, bool BUF>
+template <int G, int U, bool NT, bool BUF, int N = U>
 __device__ __forceinline__ void issue_pass(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, const Pkt &k, uint32_t c0,
-                                           uint4 (&v)[U])
+                                           uint4 (&v)[N])
 {
     const uint64_t first = k.start - static_cast<uint64_t>(k.s);  // 16-aligned offset of chunk 0
 #pragma unroll
@@ -279,8 +284,8 @@ __device__ __forceinline__ void issue_pass(const CsumArgs &a, __amdgpu_buffer_rs
     }
 }
 
-template <int G, int U>
-__device__ __forceinline__ void mask_edges(const Pkt &k, uint32_t c0, uint4 (&v)[U])
+template <int G, int U, int N = U>
+__device__ __forceinline__ void mask_edges(const Pkt &k, uint32_t c0, uint4 (&v)[N])
 {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -297,8 +302,8 @@ __device__ __forceinline__ void mask_edges(const Pkt &k, uint32_t c0, uint4 (&v)
 }
 
 // Little-endian 16-bit word sum (v_sad_u16: lo16 + hi16 + acc, one op per dword).
-template <int U>
-__device__ __forceinline__ uint32_t sum_le(const uint4 (&v)[U], uint32_t acc)
+template <int U, int N = U>
+__device__ __forceinline__ uint32_t sum_le(const uint4 (&v)[N], uint32_t acc)
 {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -311,8 +316,8 @@ __device__ __forceinline__ uint32_t sum_le(const uint4 (&v)[U], uint32_t acc)
 }
 
 // Exact big-endian word sum mod 2^32: 256 * (high-half bytes) + (low-half bytes).
-template <int U>
-__device__ __forceinline__ void sum_be(const uint4 (&v)[U], uint32_t w_hi, uint32_t &hs, uint32_t &ls)
+template <int U, int N = U>
+__device__ __forceinline__ void sum_be(const uint4 (&v)[N], uint32_t w_hi, uint32_t &hs, uint32_t &ls)
 {
     const uint32_t w_lo = w_hi ^ 0x01010101u;
 #pragma unroll
@@ -329,28 +334,28 @@ __device__ __forceinline__ void sum_be(const uint4 (&v)[U], uint32_t w_hi, uint3
 }
 
 // One packet's contribution from this lane.  `v` holds the (prefetched) first pass.
-template <int G, int U, bool NT, bool BUF>
+template <int G, int U, bool NT, bool BUF, int N = U>
 __device__ __forceinline__ uint32_t packet_partial(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, const Pkt &k,
-                                                   uint32_t sub, uint4 (&v)[U])
+                                                   uint32_t sub, uint4 (&v)[N])
 {
     constexpr uint32_t kPass = G * U;
-    mask_edges<G, U>(k, sub, v);
+    mask_edges<G, U, N>(k, sub, v);
     if (!k.big) {
-        uint32_t acc = sum_le<U>(v, 0u);
+        uint32_t acc = sum_le<U, N>(v, 0u);
         for (uint32_t c0 = kPass + sub; c0 < k.nch; c0 += kPass) {  // packets longer than one pass (reuse v)
-            issue_pass<G, U, NT, BUF>(a, rsrc, k, c0, v);
-            mask_edges<G, U>(k, c0, v);
-            acc = sum_le<U>(v, acc);
+            issue_pass<G, U, NT, BUF, N>(a, rsrc, k, c0, v);
+            mask_edges<G, U, N>(k, c0, v);
+            acc = sum_le<U, N>(v, acc);
         }
         return acc;  // LE-word sum, exact (< 2^32 for a packet of <= 128 KiB)
     }
     const uint32_t w_hi = (k.start & 1) ? 0x01000100u : 0x00010001u;
     uint32_t hs = 0, ls = 0;
-    sum_be<U>(v, w_hi, hs, ls);
+    sum_be<U, N>(v, w_hi, hs, ls);
     for (uint32_t c0 = kPass + sub; c0 < k.nch; c0 += kPass) {
-        issue_pass<G, U, NT, BUF>(a, rsrc, k, c0, v);
-        mask_edges<G, U>(k, c0, v);
-        sum_be<U>(v, w_hi, hs, ls);
+        issue_pass<G, U, NT, BUF, N>(a, rsrc, k, c0, v);
+        mask_edges<G, U, N>(k, c0, v);
+        sum_be<U, N>(v, w_hi, hs, ls);
     }
     return (hs << 8) + ls;  // BE-word sum mod 2^32, exactly the reference's accumulator
 }
@@ -467,53 +472,110 @@ struct ClassRun {
     uint32_t cnt;   // packets in the class (wave-uniform)
 };
 
-template <int G, int U, bool NT, bool BUF>
-__device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, ClassRun cr,
-                                          uint64_t s_start, uint32_t s_len, bool in_class, uint32_t rank,
-                                          uint32_t lane, uint32_t &mine)
+// Size classes (16-byte chunks a packet spans) and the shape each class runs with.
+constexpr uint32_t kNumClasses = 5;
+constexpr uint32_t kClassMax[kNumClasses - 1] = {4, 16, 64, 128};  // above the last: jumbo
+constexpr uint32_t kClassLog2G[kNumClasses] = {2, 2, 4, 5, 6};     // lanes per packet 4, 4, 16, 32, 64
+constexpr uint32_t kClassU[kNumClasses] = {1, 4, 4, 4, 4};         // chunks in flight per lane
+constexpr int kUMax = 4;
+
+// Round 0 of class n (wave-uniform; kNumClasses = none), issued with the class's
+// runtime shape into the shared buffer: the last round of the previous class
+// calls this, so a class starts with its first pass already in flight.
+template <bool NT, bool BUF>
+__device__ __forceinline__ Pkt prefetch_class(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint32_t n,
+                                              const ClassRun (&cr)[kNumClasses], uint64_t s_start, uint32_t s_len,
+                                              uint32_t lane, uint4 (&w)[kUMax])
 {
+    uint32_t lg = 6, U = 0, off = 0, cnt = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < kNumClasses; ++c)
+        if (n == c) {
+            lg = kClassLog2G[c];
+            U = kClassU[c];
+            off = cr[c].off;
+            cnt = cr[c].cnt;
+        }
+    const uint32_t G = 1u << lg;
+    const uint32_t sub = lane & (G - 1);
+    const uint32_t grp = lane >> lg;
+    const bool valid = grp < cnt;
+    const int src = static_cast<int>(off + (valid ? grp : 0u));
+    const uint32_t lo = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(s_start)), src, 64));
+    const uint32_t hi = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(s_start >> 32)), src, 64));
+    const uint32_t L = static_cast<uint32_t>(__shfl(static_cast<int>(s_len), src, 64));
+    Pkt k = make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L);
+    k.nch = valid ? k.nch : 0u;
+    const uint64_t first = k.start - static_cast<uint64_t>(k.s);
+#pragma unroll
+    for (int u = 0; u < kUMax; ++u) {
+        const uint32_t c = sub + u * G;
+        const bool in = static_cast<uint32_t>(u) < U && c < k.nch;
+        if constexpr (BUF) {
+            const uint32_t o = in ? static_cast<uint32_t>(first + (static_cast<uint64_t>(c) << 4)) : kOobOffset;
+            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, NT ? 2 : 0);
+            w[u] = make_uint4(x.x, x.y, x.z, x.w);
+        } else {
+            const uint4 x = load_chunk<NT>(a.arena + first + (in ? (static_cast<uint64_t>(c) << 4) : 0));
+            w[u] = in ? x : make_uint4(0, 0, 0, 0);
+        }
+    }
+    return k;
+}
+
+// All rounds of class C.  On entry (cur, v) hold round 0's prefetched first pass;
+// on exit they hold the first pass of class `next` (the next non-empty class).
+template <uint32_t C, bool NT, bool BUF>
+__device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc,
+                                          const ClassRun (&cr)[kNumClasses], uint32_t next, uint64_t s_start,
+                                          uint32_t s_len, bool in_class, uint32_t rank, uint32_t lane, Pkt &cur,
+                                          uint4 (&v)[kUMax], uint32_t &mine)
+{
+    constexpr int G = 1 << kClassLog2G[C];
+    constexpr int U = static_cast<int>(kClassU[C]);
     constexpr uint32_t P = 64 / G;
     const uint32_t sub = lane & (G - 1);
     const uint32_t grp = lane / G;
-    const uint32_t rounds = (cr.cnt + P - 1) / P;
+    const uint32_t rounds = (cr[C].cnt + P - 1) / P;
     if (rounds == 0)
-        return;
-    // group `grp` of round r takes sorted position off + r*P + grp (if inside the class)
-    auto fetch = [&](uint32_t r) {
+        return;  // (cur, v) already hold the next class's prefetch
+    auto fetch = [&](uint32_t r) {  // group `grp` of round r: sorted position off + r*P + grp
         const uint32_t i = r * P + grp;
-        Pkt k = fetch_pkt<G>(s_start, s_len, cr.off + (i < cr.cnt ? i : 0));
-        k.nch = (i < cr.cnt) ? k.nch : 0u;
+        Pkt k = fetch_pkt<G>(s_start, s_len, cr[C].off + (i < cr[C].cnt ? i : 0));
+        k.nch = (i < cr[C].cnt) ? k.nch : 0u;
         return k;
     };
-    Pkt cur = fetch(0);
-    uint4 v[U];
-    issue_pass<G, U, NT, BUF>(a, rsrc, cur, sub, v);
-    for (uint32_t r = 0; r < rounds; ++r) {
-        const bool has_next = r + 1 < rounds;
-        Pkt nxt = fetch(has_next ? r + 1 : r);
-        nxt.nch = has_next ? nxt.nch : 0u;
-        uint4 w[U];
-        issue_pass<G, U, NT, BUF>(a, rsrc, nxt, sub, w);  // prefetch: see csum_rounds_kernel
-        const uint32_t words = group_allreduce<G>(packet_partial<G, U, NT, BUF>(a, rsrc, cur, sub, v));
+    auto finish = [&](uint32_t r) {  // consume round r from (cur, v), route each sum to its owner lane
+        const uint32_t words = group_allreduce<G>(packet_partial<G, U, NT, BUF, kUMax>(a, rsrc, cur, sub, v));
         if constexpr (G == 64) {
-            const uint32_t t = words;  // wave-uniform
-            mine = (in_class && rank == r) ? t : mine;
+            mine = (in_class && rank == r) ? words : mine;  // wave-uniform sum
         } else {
-            const uint32_t t = static_cast<uint32_t>(__shfl(static_cast<int>(words), static_cast<int>((rank % P) * G), 64));
+            const uint32_t t =
+                static_cast<uint32_t>(__shfl(static_cast<int>(words), static_cast<int>((rank % P) * G), 64));
             mine = (in_class && rank / P == r) ? t : mine;
         }
+    };
+    for (uint32_t r = 0; r + 1 < rounds; ++r) {
+        const Pkt nxt = fetch(r + 1);
+        uint4 w[kUMax];
+        issue_pass<G, U, NT, BUF, kUMax>(a, rsrc, nxt, sub, w);  // in-class prefetch (vmcnt stays exact)
+        finish(r);
         cur = nxt;
 #pragma unroll
         for (int u = 0; u < U; ++u)
             v[u] = w[u];
     }
+    uint4 w[kUMax];
+    const Pkt nxt = prefetch_class<NT, BUF>(a, rsrc, next, cr, s_start, s_len, lane, w);  // cross-class prefetch
+    finish(rounds - 1);
+    cur = nxt;
+#pragma unroll
+    for (int u = 0; u < kUMax; ++u)
+        v[u] = w[u];
 }
 
-// Size classes (in 16-byte chunks a packet spans) and the shape each runs with.
-constexpr uint32_t kClassMax[4] = {4, 16, 64, 128};  // tiny, small, medium, large; above: jumbo
-
 template <bool STRIDED, bool NT, bool BUF>
-__global__ __launch_bounds__(kBlock) void csum_mixed_kernel(const CsumArgs a)
+__global__ __launch_bounds__(kBlock, BUF ? 4 : 3) void csum_mixed_kernel(const CsumArgs a)  // BUF: <= 128 VGPRs
 {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
@@ -542,15 +604,16 @@ __global__ __launch_bounds__(kBlock) void csum_mixed_kernel(const CsumArgs a)
             d_len = 0;
             d_start = 0;
         }
-        // size class of this lane's packet
+        // size class of this lane's packet; ranks within the class; sorted position
         const uint32_t nch = d_len ? static_cast<uint32_t>(((d_start & 15) + d_len + 15) >> 4) : 0u;
-        const uint32_t cls = (nch <= kClassMax[0]) ? 0u : (nch <= kClassMax[1]) ? 1u
-                           : (nch <= kClassMax[2]) ? 2u : (nch <= kClassMax[3]) ? 3u : 4u;
-        uint32_t pos = 0, rank = 0;
-        ClassRun cr[5];
-        uint32_t off = 0;
+        uint32_t cls = kNumClasses - 1;
 #pragma unroll
-        for (uint32_t c = 0; c < 5; ++c) {
+        for (int c = kNumClasses - 2; c >= 0; --c)
+            cls = (nch <= kClassMax[c]) ? static_cast<uint32_t>(c) : cls;
+        uint32_t pos = 0, rank = 0, off = 0;
+        ClassRun cr[kNumClasses];
+#pragma unroll
+        for (uint32_t c = 0; c < kNumClasses; ++c) {
             const uint64_t m = __ballot(cls == c);
             const uint32_t below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
                                                              __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
@@ -561,22 +624,29 @@ __global__ __launch_bounds__(kBlock) void csum_mixed_kernel(const CsumArgs a)
             cr[c] = ClassRun{off, static_cast<uint32_t>(__popcll(m))};
             off += cr[c].cnt;
         }
+        // next non-empty class after each class (wave-uniform); kNumClasses = none
+        uint32_t next[kNumClasses + 1];
+        next[kNumClasses] = kNumClasses;
+#pragma unroll
+        for (int c = kNumClasses - 1; c >= 0; --c)
+            next[c] = cr[c].cnt ? static_cast<uint32_t>(c) : next[c + 1];
         // sort the descriptors by class: lane `pos` receives this lane's packet
-        const uint32_t addr = pos * 4;
+        const int addr = static_cast<int>(pos * 4);
         const uint32_t s_lo = static_cast<uint32_t>(
-            __builtin_amdgcn_ds_permute(static_cast<int>(addr), static_cast<int>(static_cast<uint32_t>(d_start))));
+            __builtin_amdgcn_ds_permute(addr, static_cast<int>(static_cast<uint32_t>(d_start))));
         const uint32_t s_hi = static_cast<uint32_t>(
-            __builtin_amdgcn_ds_permute(static_cast<int>(addr), static_cast<int>(static_cast<uint32_t>(d_start >> 32))));
-        const uint32_t s_len = static_cast<uint32_t>(
-            __builtin_amdgcn_ds_permute(static_cast<int>(addr), static_cast<int>(d_len)));
+            __builtin_amdgcn_ds_permute(addr, static_cast<int>(static_cast<uint32_t>(d_start >> 32))));
+        const uint32_t s_len = static_cast<uint32_t>(__builtin_amdgcn_ds_permute(addr, static_cast<int>(d_len)));
         const uint64_t s_start = (static_cast<uint64_t>(s_hi) << 32) | s_lo;
 
         uint32_t mine = 0;
-        run_class<4, 1, NT, BUF>(a, rsrc, cr[0], s_start, s_len, cls == 0, rank, lane, mine);
-        run_class<4, 4, NT, BUF>(a, rsrc, cr[1], s_start, s_len, cls == 1, rank, lane, mine);
-        run_class<16, 4, NT, BUF>(a, rsrc, cr[2], s_start, s_len, cls == 2, rank, lane, mine);
-        run_class<32, 4, NT, BUF>(a, rsrc, cr[3], s_start, s_len, cls == 3, rank, lane, mine);
-        run_class<64, 4, NT, BUF>(a, rsrc, cr[4], s_start, s_len, cls == 4, rank, lane, mine);
+        uint4 v[kUMax];
+        Pkt cur = prefetch_class<NT, BUF>(a, rsrc, next[0], cr, s_start, s_len, lane, v);
+        run_class<0, NT, BUF>(a, rsrc, cr, next[1], s_start, s_len, cls == 0, rank, lane, cur, v, mine);
+        run_class<1, NT, BUF>(a, rsrc, cr, next[2], s_start, s_len, cls == 1, rank, lane, cur, v, mine);
+        run_class<2, NT, BUF>(a, rsrc, cr, next[3], s_start, s_len, cls == 2, rank, lane, cur, v, mine);
+        run_class<3, NT, BUF>(a, rsrc, cr, next[4], s_start, s_len, cls == 3, rank, lane, cur, v, mine);
+        run_class<4, NT, BUF>(a, rsrc, cr, next[5], s_start, s_len, cls == 4, rank, lane, cur, v, mine);
 
         const uint16_t res = finalize(mine, d_start, d_len, d_seed, d_ok, a.flags);
         if (live)

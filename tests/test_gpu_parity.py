@@ -217,3 +217,27 @@ def test_host_resident_pipeline(oracle, pinned):
     hb.close()
     if pinned:
         pb.free()
+
+
+def test_arena_beyond_4gib_uses_64bit_path(oracle):
+    """Arenas >= 4 GiB cannot use 32-bit buffer offsets: every kernel takes its
+    64-bit global-load path.  Packets straddle the 4 GiB line and sit at both ends."""
+    nbytes = (4 << 30) + (64 << 20)
+    arena = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+    fill_splitmix64(arena, 0xB16)
+    four_g = 1 << 32
+    rows = []
+    for base in (0, four_g - 6000, four_g - 1, four_g + 3, nbytes - 12000):
+        for i, L in enumerate((1, 40, 576, 1500, 9000, 3)):
+            rows.append((base + 1700 * i + (i % 3), L))
+    off = np.array([r[0] for r in rows], dtype=np.uint64)
+    ln = np.array([r[1] for r in rows], dtype=np.uint32)
+    sd = (O.splitmix64_words(77, len(rows)) & np.uint64(0xFFFF)).astype(np.uint16)
+    # expected values from host copies of only the touched windows
+    expect = np.array([oracle.compute_ones_comp(int(s), arena[int(o):int(o) + int(L)].cpu().numpy().tobytes())
+                       for o, L, s in zip(off, ln, sd)], dtype=np.uint16)
+    d = dev_desc(off, ln, sd)
+    for shape in (None, (0, 16, 2, 0), (2, 64, 4, 0), (1, 16, 4, 0), (3, 32, 4, 0), (4, 0, 0, 0), (6, 0, 0, 0)):
+        assert np.array_equal(host_u16(csum_batch(arena, *d, shape=shape)), expect), shape
+    del arena
+    torch.cuda.empty_cache()
