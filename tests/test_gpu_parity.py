@@ -227,12 +227,13 @@ def test_arena_beyond_4gib_uses_64bit_path(oracle):
     fill_splitmix64(arena, 0xB16)
     four_g = 1 << 32
     rows = []
-    for base in (0, four_g - 6000, four_g - 1, four_g + 3, nbytes - 12000):
+    for base in (0, four_g - 6000, four_g - 1, four_g + 3, nbytes - 20000):   # every packet inside the arena
         for i, L in enumerate((1, 40, 576, 1500, 9000, 3)):
             rows.append((base + 1700 * i + (i % 3), L))
     off = np.array([r[0] for r in rows], dtype=np.uint64)
     ln = np.array([r[1] for r in rows], dtype=np.uint32)
     sd = (O.splitmix64_words(77, len(rows)) & np.uint64(0xFFFF)).astype(np.uint16)
+    assert int((off + ln).max()) <= nbytes
     # expected values from host copies of only the touched windows
     expect = np.array([oracle.compute_ones_comp(int(s), arena[int(o):int(o) + int(L)].cpu().numpy().tobytes())
                        for o, L, s in zip(off, ln, sd)], dtype=np.uint16)
