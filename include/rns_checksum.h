@@ -115,6 +115,34 @@ int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uin
                                uint64_t stride, uint32_t len, const uint16_t *d_seed, uint16_t *d_out,
                                uint32_t n, uint32_t flags, uint32_t *d_bad, void *stream);
 
+/* Fragment chains: util.rs:112 `compute_buffer_ones_comp` for a batch of
+ * NetBuffer-style fragment lists (buf.rs:466-487).  Packet i is fragments
+ * [d_first[i], d_first[i+1]) of (d_frag_off, d_frag_len) — d_first has n_pkts+1
+ * entries; each fragment is folded on its own, so an odd-length non-final
+ * fragment is zero-padded exactly like the per-fragment call.  d_frag_sums is
+ * device scratch of n_frags u16 (receives compute_ones_comp(0, fragment)).
+ * A packet with a fragment outside the arena gets 0 and is counted in *d_bad.
+ * Exact for fragments up to 128 KiB (NetBuffer fragments are 512 B, buf.rs:50);
+ * an empty fragment contributes nothing (the reference panics on it). */
+int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_frag_off,
+                       const uint32_t *d_frag_len, uint32_t n_frags, const uint32_t *d_first,
+                       const uint16_t *d_seed, uint16_t *d_out, uint32_t n_pkts, uint32_t flags,
+                       uint32_t frag_len_hint, uint16_t *d_frag_sums, uint32_t *d_bad, void *stream);
+
+/* Transmit in-place fill (tcp.rs:957-973, udp.rs:158-171, icmp.rs:87-112,
+ * ip.rs:158-159): for packet i, sum d_arena[d_off[i] .. + d_len[i]) seeded with
+ * d_seed[i], counting the 2-byte checksum field at packet offset d_field[i]
+ * (d_field == NULL => field_off for every packet: TCP 16, UDP 6, ICMP 2, IPv4
+ * header 10) as zero — the reference zero-fills it (buf.rs:286-288) — and store
+ * the result (0xffff ^ sum with RNS_FLAG_COMPLEMENT, as every call site does)
+ * big-endian into the field (set_be16).  UDP keeps the reference's behaviour of
+ * storing 0 as-is (no RFC 768 0 -> 0xffff).  d_out (optional) also receives the
+ * results.  Packets must not overlap.  A packet outside the arena or too short
+ * for its field is left untouched, gets d_out 0, and is counted in *d_bad. */
+int rns_csum_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off, const uint32_t *d_len,
+                      const uint16_t *d_seed, const uint16_t *d_field, uint32_t field_off, uint16_t *d_out,
+                      uint32_t n, uint32_t flags, uint32_t *d_bad, void *stream);
+
 /* Tuning entry (bench / tests): explicit kernel shape.  variant bit 0: 0 = group
  * kernel (one lane stores each result), 1 = rounds kernel (a wave owns 64
  * consecutive packets, one coalesced result store); bit 1: nontemporal packet

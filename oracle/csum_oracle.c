@@ -183,3 +183,22 @@ double oracle_time_ones_comp(const uint8_t *buf, size_t len, uint64_t iters)
     (void)sink;
     return ((double)(t1.tv_sec - t0.tv_sec) * 1e9 + (double)(t1.tv_nsec - t0.tv_nsec)) / (double)(iters ? iters : 1);
 }
+
+/*
+ * Batch of fragment chains: packet i = fragments [first[i], first[i+1]) of
+ * (frag_off, frag_len) in `arena`, folded one after another from seed[i]
+ * (util.rs:112-119 over BufferIterator's slices, buf.rs:466-487).  An empty
+ * fragment would panic in the reference; here it leaves the sum unchanged, the
+ * behaviour the product API defines (tests mark it "parity unpinned").
+ */
+void oracle_chain_batch(const uint8_t *arena, const uint64_t *frag_off, const uint32_t *frag_len,
+                        const uint32_t *first, const uint16_t *seed, uint16_t *out, size_t npkts, int complement)
+{
+    for (size_t i = 0; i < npkts; i++) {
+        int32_t sum = seed ? seed[i] : 0;
+        for (uint32_t f = first[i]; f < first[i + 1]; f++)
+            if (frag_len[f])
+                sum = oracle_compute_ones_comp((uint16_t)sum, arena + frag_off[f], frag_len[f]);
+        out[i] = (uint16_t)(complement ? (0xffff ^ (uint32_t)sum) : (uint32_t)sum);
+    }
+}

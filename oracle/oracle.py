@@ -137,6 +137,8 @@ class Oracle:
         L.oracle_batch.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_int]
         L.oracle_batch_mt.restype = ctypes.c_int
         L.oracle_batch_mt.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
+        L.oracle_chain_batch.restype = None
+        L.oracle_chain_batch.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_size_t, ctypes.c_int]
         L.oracle_time_ones_comp.restype = ctypes.c_double
         L.oracle_time_ones_comp.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]
 
@@ -190,6 +192,25 @@ class Oracle:
                 raise RuntimeError("oracle_batch_mt: thread creation failed")
         return out
 
+
+    def chain_batch(self, arena: np.ndarray, frag_off: np.ndarray, frag_len: np.ndarray, first: np.ndarray,
+                    seed: np.ndarray | None, complement: bool = False) -> np.ndarray:
+        """compute_buffer_ones_comp per packet over fragment chains (CSR `first`)."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        frag_off = np.ascontiguousarray(frag_off, dtype=np.uint64)
+        frag_len = np.ascontiguousarray(frag_len, dtype=np.uint32)
+        first = np.ascontiguousarray(first, dtype=np.uint32)
+        n = first.shape[0] - 1
+        if frag_off.shape[0] and int((frag_off + frag_len.astype(np.uint64)).max()) > arena.shape[0]:
+            raise ValueError("fragment out of arena bounds")
+        out = np.empty(n, dtype=np.uint16)
+        sp = None
+        if seed is not None:
+            seed = np.ascontiguousarray(seed, dtype=np.uint16)
+            sp = seed.ctypes.data
+        self.lib.oracle_chain_batch(arena.ctypes.data, frag_off.ctypes.data, frag_len.ctypes.data, first.ctypes.data,
+                                    sp, out.ctypes.data, n, int(complement))
+        return out
 
     def time_ones_comp(self, data: bytes, iters: int) -> float:
         """ns per compute_ones_comp(0, data) call (benches/util_bench.rs:20-45 equivalent)."""

@@ -149,6 +149,83 @@ def csum_batch_strided(arena: torch.Tensor, n: int, stride: int, length: int, *,
     return out
 
 
+def csum_chain(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch.Tensor, first: torch.Tensor,
+               seed: torch.Tensor | None = None, *, complement: bool = False, out: torch.Tensor | None = None,
+               frag_sums: torch.Tensor | None = None, bad: torch.Tensor | None = None,
+               frag_len_hint: int = 512) -> torch.Tensor:
+    """util.rs:112 ``compute_buffer_ones_comp`` for a batch of fragment chains.
+
+    Packet i = fragments ``first[i] .. first[i+1]`` (``first``: int32 [n+1]) of
+    ``(frag_off, frag_len)``; each fragment is folded on its own like the reference.
+    """
+    _require_cuda(arena, "arena", (torch.uint8,))
+    _require_cuda(frag_off, "frag_off", (torch.int64,))
+    _require_cuda(frag_len, "frag_len", (torch.int32,))
+    _require_cuda(first, "first", (torch.int32,))
+    nf = frag_off.numel()
+    n = first.numel() - 1
+    if frag_len.numel() != nf or n < 0:
+        raise ValueError("frag_off/frag_len sizes differ or first is empty")
+    dev = arena.device
+    seed_ptr = None
+    if seed is not None:
+        _require_cuda(seed, "seed", _U16)
+        if seed.numel() != n:
+            raise ValueError("seed must have one entry per packet")
+        seed_ptr = seed.data_ptr()
+    if out is None:
+        out = torch.empty(max(n, 0), dtype=torch.uint16, device=dev)
+    if frag_sums is None:
+        frag_sums = torch.empty(max(nf, 1), dtype=torch.uint16, device=dev)
+    bad_ptr = bad.data_ptr() if bad is not None else None
+    lib = _lib.load()
+    with torch.cuda.device(dev):
+        st = lib.rns_csum_chain_dev(arena.data_ptr(), arena.numel(), frag_off.data_ptr(), frag_len.data_ptr(), nf,
+                                    first.data_ptr(), seed_ptr, out.data_ptr(), n,
+                                    _lib.RNS_FLAG_COMPLEMENT if complement else 0, frag_len_hint,
+                                    frag_sums.data_ptr(), bad_ptr, _stream_handle(dev))
+    _lib.check(st, "rns_csum_chain_dev")
+    return out
+
+
+def csum_fill(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, seed: torch.Tensor | None = None, *,
+              field: torch.Tensor | None = None, field_off: int = 16, complement: bool = True,
+              out: torch.Tensor | None = None, bad: torch.Tensor | None = None) -> torch.Tensor | None:
+    """Transmit in-place fill: each packet's checksum, computed with its 2-byte field
+    counted as zero, is stored big-endian into the field (tcp.rs:970-973 ``set_be16``).
+
+    ``field`` (int16/uint16 [n]) gives per-packet field offsets, else ``field_off``
+    for all (TCP 16, UDP 6, ICMP 2, IPv4 header 10).  Returns ``out`` if given.
+    """
+    _require_cuda(arena, "arena", (torch.uint8,))
+    _require_cuda(off, "off", (torch.int64,))
+    _require_cuda(length, "length", (torch.int32,))
+    n = off.numel()
+    if length.numel() != n:
+        raise ValueError("off and length must have the same number of packets")
+    dev = arena.device
+    ptrs = []
+    for name, t in (("seed", seed), ("field", field), ("out", out)):
+        if t is None:
+            ptrs.append(None)
+            continue
+        _require_cuda(t, name, _U16)
+        if t.numel() != n or t.device != dev:
+            raise ValueError(f"{name} must have one entry per packet on the arena's device")
+        ptrs.append(t.data_ptr())
+    bad_ptr = None
+    if bad is not None:
+        _require_cuda(bad, "bad", (torch.int32,))
+        bad_ptr = bad.data_ptr()
+    lib = _lib.load()
+    with torch.cuda.device(dev):
+        st = lib.rns_csum_fill_dev(arena.data_ptr(), arena.numel(), off.data_ptr(), length.data_ptr(), ptrs[0],
+                                   ptrs[1], int(field_off), ptrs[2], n,
+                                   _lib.RNS_FLAG_COMPLEMENT if complement else 0, bad_ptr, _stream_handle(dev))
+    _lib.check(st, "rns_csum_fill_dev")
+    return out
+
+
 def fill_splitmix64(buf: torch.Tensor, seed: int) -> torch.Tensor:
     """Fill a device uint8 buffer with the splitmix64 byte stream (same bytes as
     oracle.splitmix64_bytes(seed, n))."""

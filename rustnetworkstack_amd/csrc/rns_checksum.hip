@@ -53,6 +53,8 @@ struct CsumArgs {
     uint32_t fixed_len;
     uint32_t n;
     uint32_t flags;
+    const uint16_t *field;     // transmit fill: per-packet checksum field offset (null => field_off)
+    uint32_t field_off;
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -235,12 +237,17 @@ struct Pkt {
     int s;                // first valid byte in chunk 0
     int e;                // bytes valid in the last chunk (1..16)
     bool big;             // > kNoWrapBytes: exact big-endian path
+    int hole;             // transmit fill: the 2-byte checksum field, as a byte index from
+                          // chunk 0's first byte (counted as zero while summing); kNoHole: none
 };
 
-__device__ __forceinline__ Pkt make_pkt(uint64_t start, uint32_t L)
+constexpr int kNoHole = -4096;
+
+__device__ __forceinline__ Pkt make_pkt(uint64_t start, uint32_t L, uint32_t field = 0xFFFFFFFFu)
 {
     Pkt k;
     k.start = start;
+    k.hole = (field < L) ? static_cast<int>(start & 15) + static_cast<int>(field) : kNoHole;
     k.s = static_cast<int>(k.start & 15);
     const uint64_t span = static_cast<uint64_t>(k.s) + L;
     k.nch = L ? static_cast<uint32_t>((span + 15) >> 4) : 0u;
@@ -249,13 +256,14 @@ __device__ __forceinline__ Pkt make_pkt(uint64_t start, uint32_t L)
     return k;
 }
 
-template <int G>
-__device__ __forceinline__ Pkt fetch_pkt(uint64_t d_start, uint32_t d_len, uint32_t src)
+template <int G, bool HOLE = false>
+__device__ __forceinline__ Pkt fetch_pkt(uint64_t d_start, uint32_t d_len, uint32_t src, uint32_t d_field = 0xFFFFFFFFu)
 {
     const uint32_t lo = bcast_from<G>(static_cast<uint32_t>(d_start), src);
     const uint32_t hi = bcast_from<G>(static_cast<uint32_t>(d_start >> 32), src);
     const uint32_t L = bcast_from<G>(d_len, src);
-    return make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L);
+    const uint32_t f = HOLE ? bcast_from<G>(d_field, src) : 0xFFFFFFFFu;
+    return make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L, f);
 }
 
 // Loads of one pass: chunk c = c0 + u*G of the packet, for u < U.  Branch-free:
@@ -284,7 +292,17 @@ __device__ __forceinline__ void issue_pass(const CsumArgs &a, __amdgpu_buffer_rs
     }
 }
 
-template <int G, int U, int N = U>
+// Zero bytes [lo, hi) of the 4-byte dword at byte j4 of a 16-byte chunk.
+__device__ __forceinline__ uint32_t drop_bytes(uint32_t d, int lo, int hi, int j4)
+{
+    const int a = min(max(lo - j4, 0), 4);
+    const int b = min(max(hi - j4, 0), 4);
+    const uint32_t hm = static_cast<uint32_t>((1ull << (8 * b)) - 1);
+    const uint32_t lm = static_cast<uint32_t>((1ull << (8 * a)) - 1);
+    return d & ~(hm & ~lm);
+}
+
+template <int G, int U, int N = U, bool HOLE = false>
 __device__ __forceinline__ void mask_edges(const Pkt &k, uint32_t c0, uint4 (&v)[N])
 {
 #pragma unroll
@@ -297,6 +315,15 @@ __device__ __forceinline__ void mask_edges(const Pkt &k, uint32_t c0, uint4 (&v)
             v[u].y = keep_bytes(v[u].y, lo, hi, 4);
             v[u].z = keep_bytes(v[u].z, lo, hi, 8);
             v[u].w = keep_bytes(v[u].w, lo, hi, 12);
+        }
+        if constexpr (HOLE) {  // the checksum field counts as zero (alloc_header zero-fills it, buf.rs:286-288)
+            const int hp = k.hole - 16 * static_cast<int>(c);
+            if (hp > -2 && hp < 16) {
+                v[u].x = drop_bytes(v[u].x, hp, hp + 2, 0);
+                v[u].y = drop_bytes(v[u].y, hp, hp + 2, 4);
+                v[u].z = drop_bytes(v[u].z, hp, hp + 2, 8);
+                v[u].w = drop_bytes(v[u].w, hp, hp + 2, 12);
+            }
         }
     }
 }
@@ -334,17 +361,17 @@ __device__ __forceinline__ void sum_be(const uint4 (&v)[N], uint32_t w_hi, uint3
 }
 
 // One packet's contribution from this lane.  `v` holds the (prefetched) first pass.
-template <int G, int U, bool NT, bool BUF, int N = U>
+template <int G, int U, bool NT, bool BUF, int N = U, bool HOLE = false>
 __device__ __forceinline__ uint32_t packet_partial(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, const Pkt &k,
                                                    uint32_t sub, uint4 (&v)[N])
 {
     constexpr uint32_t kPass = G * U;
-    mask_edges<G, U, N>(k, sub, v);
+    mask_edges<G, U, N, HOLE>(k, sub, v);
     if (!k.big) {
         uint32_t acc = sum_le<U, N>(v, 0u);
         for (uint32_t c0 = kPass + sub; c0 < k.nch; c0 += kPass) {  // packets longer than one pass (reuse v)
             issue_pass<G, U, NT, BUF, N>(a, rsrc, k, c0, v);
-            mask_edges<G, U, N>(k, c0, v);
+            mask_edges<G, U, N, HOLE>(k, c0, v);
             acc = sum_le<U, N>(v, acc);
         }
         return acc;  // LE-word sum, exact (< 2^32 for a packet of <= 128 KiB)
@@ -354,7 +381,7 @@ __device__ __forceinline__ uint32_t packet_partial(const CsumArgs &a, __amdgpu_b
     sum_be<U, N>(v, w_hi, hs, ls);
     for (uint32_t c0 = kPass + sub; c0 < k.nch; c0 += kPass) {
         issue_pass<G, U, NT, BUF, N>(a, rsrc, k, c0, v);
-        mask_edges<G, U, N>(k, c0, v);
+        mask_edges<G, U, N, HOLE>(k, c0, v);
         sum_be<U, N>(v, w_hi, hs, ls);
     }
     return (hs << 8) + ls;  // BE-word sum mod 2^32, exactly the reference's accumulator
@@ -482,10 +509,10 @@ constexpr int kUMax = 4;
 // Round 0 of class n (wave-uniform; kNumClasses = none), issued with the class's
 // runtime shape into the shared buffer: the last round of the previous class
 // calls this, so a class starts with its first pass already in flight.
-template <bool NT, bool BUF>
+template <bool NT, bool BUF, bool FILL>
 __device__ __forceinline__ Pkt prefetch_class(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint32_t n,
                                               const ClassRun (&cr)[kNumClasses], uint64_t s_start, uint32_t s_len,
-                                              uint32_t lane, uint4 (&w)[kUMax])
+                                              uint32_t s_field, uint32_t lane, uint4 (&w)[kUMax])
 {
     uint32_t lg = 6, U = 0, off = 0, cnt = 0;
 #pragma unroll
@@ -504,7 +531,8 @@ __device__ __forceinline__ Pkt prefetch_class(const CsumArgs &a, __amdgpu_buffer
     const uint32_t lo = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(s_start)), src, 64));
     const uint32_t hi = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(s_start >> 32)), src, 64));
     const uint32_t L = static_cast<uint32_t>(__shfl(static_cast<int>(s_len), src, 64));
-    Pkt k = make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L);
+    const uint32_t f = FILL ? static_cast<uint32_t>(__shfl(static_cast<int>(s_field), src, 64)) : 0xFFFFFFFFu;
+    Pkt k = make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L, f);
     k.nch = valid ? k.nch : 0u;
     const uint64_t first = k.start - static_cast<uint64_t>(k.s);
 #pragma unroll
@@ -525,11 +553,11 @@ __device__ __forceinline__ Pkt prefetch_class(const CsumArgs &a, __amdgpu_buffer
 
 // All rounds of class C.  On entry (cur, v) hold round 0's prefetched first pass;
 // on exit they hold the first pass of class `next` (the next non-empty class).
-template <uint32_t C, bool NT, bool BUF>
+template <uint32_t C, bool NT, bool BUF, bool FILL>
 __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc,
                                           const ClassRun (&cr)[kNumClasses], uint32_t next, uint64_t s_start,
-                                          uint32_t s_len, bool in_class, uint32_t rank, uint32_t lane, Pkt &cur,
-                                          uint4 (&v)[kUMax], uint32_t &mine)
+                                          uint32_t s_len, uint32_t s_field, bool in_class, uint32_t rank,
+                                          uint32_t lane, Pkt &cur, uint4 (&v)[kUMax], uint32_t &mine)
 {
     constexpr int G = 1 << kClassLog2G[C];
     constexpr int U = static_cast<int>(kClassU[C]);
@@ -541,12 +569,13 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
         return;  // (cur, v) already hold the next class's prefetch
     auto fetch = [&](uint32_t r) {  // group `grp` of round r: sorted position off + r*P + grp
         const uint32_t i = r * P + grp;
-        Pkt k = fetch_pkt<G>(s_start, s_len, cr[C].off + (i < cr[C].cnt ? i : 0));
+        Pkt k = fetch_pkt<G, FILL>(s_start, s_len, cr[C].off + (i < cr[C].cnt ? i : 0), s_field);
         k.nch = (i < cr[C].cnt) ? k.nch : 0u;
         return k;
     };
     auto finish = [&](uint32_t r) {  // consume round r from (cur, v), route each sum to its owner lane
-        const uint32_t words = group_allreduce<G>(packet_partial<G, U, NT, BUF, kUMax>(a, rsrc, cur, sub, v));
+        const uint32_t words =
+            group_allreduce<G>(packet_partial<G, U, NT, BUF, kUMax, FILL>(a, rsrc, cur, sub, v));
         if constexpr (G == 64) {
             mine = (in_class && rank == r) ? words : mine;  // wave-uniform sum
         } else {
@@ -566,7 +595,7 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
             v[u] = w[u];
     }
     uint4 w[kUMax];
-    const Pkt nxt = prefetch_class<NT, BUF>(a, rsrc, next, cr, s_start, s_len, lane, w);  // cross-class prefetch
+    const Pkt nxt = prefetch_class<NT, BUF, FILL>(a, rsrc, next, cr, s_start, s_len, s_field, lane, w);
     finish(rounds - 1);
     cur = nxt;
 #pragma unroll
@@ -574,8 +603,12 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
         v[u] = w[u];
 }
 
-template <bool STRIDED, bool NT, bool BUF>
-__global__ __launch_bounds__(kBlock, BUF ? 4 : 3) void csum_mixed_kernel(const CsumArgs a)  // BUF: <= 128 VGPRs
+// FILL (transmit in-place fill, tcp.rs:957-973 / udp.rs:158-171 / icmp.rs:87-112 /
+// ip.rs:158-159): the 2-byte checksum field of each packet counts as zero while
+// summing, and the owner lane stores the (complemented) result into it, big-endian
+// (set_be16, util.rs:132-135), after the whole wave has read its 64 packets.
+template <bool STRIDED, bool NT, bool BUF, bool FILL>
+__global__ __launch_bounds__(kBlock, (BUF && !FILL) ? 4 : 3) void csum_mixed_kernel(const CsumArgs a)  // <= 128 VGPRs
 {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
@@ -599,7 +632,13 @@ __global__ __launch_bounds__(kBlock, BUF ? 4 : 3) void csum_mixed_kernel(const C
             d_seed = a.seed ? a.seed[p] : 0u;
         }
         d_start += a.base_adjust;
-        const bool d_ok = d_start <= a.arena_bytes && d_len <= a.arena_bytes - d_start;
+        uint32_t d_field = 0xFFFFFFFFu;
+        bool d_ok = d_start <= a.arena_bytes && d_len <= a.arena_bytes - d_start;
+        if constexpr (FILL) {
+            d_field = live ? (a.field ? static_cast<uint32_t>(a.field[p]) : a.field_off) : 0u;
+            d_ok = d_ok && d_len >= 2 && d_field <= d_len - 2;  // header[f..f+2] must exist
+        }
+        const uint64_t own_start = d_start;
         if (!d_ok || d_len == 0) {
             d_len = 0;
             d_start = 0;
@@ -638,24 +677,79 @@ __global__ __launch_bounds__(kBlock, BUF ? 4 : 3) void csum_mixed_kernel(const C
             __builtin_amdgcn_ds_permute(addr, static_cast<int>(static_cast<uint32_t>(d_start >> 32))));
         const uint32_t s_len = static_cast<uint32_t>(__builtin_amdgcn_ds_permute(addr, static_cast<int>(d_len)));
         const uint64_t s_start = (static_cast<uint64_t>(s_hi) << 32) | s_lo;
+        const uint32_t s_field =
+            FILL ? static_cast<uint32_t>(__builtin_amdgcn_ds_permute(addr, static_cast<int>(d_field))) : 0u;
 
         uint32_t mine = 0;
         uint4 v[kUMax];
-        Pkt cur = prefetch_class<NT, BUF>(a, rsrc, next[0], cr, s_start, s_len, lane, v);
-        run_class<0, NT, BUF>(a, rsrc, cr, next[1], s_start, s_len, cls == 0, rank, lane, cur, v, mine);
-        run_class<1, NT, BUF>(a, rsrc, cr, next[2], s_start, s_len, cls == 1, rank, lane, cur, v, mine);
-        run_class<2, NT, BUF>(a, rsrc, cr, next[3], s_start, s_len, cls == 2, rank, lane, cur, v, mine);
-        run_class<3, NT, BUF>(a, rsrc, cr, next[4], s_start, s_len, cls == 3, rank, lane, cur, v, mine);
-        run_class<4, NT, BUF>(a, rsrc, cr, next[5], s_start, s_len, cls == 4, rank, lane, cur, v, mine);
+        Pkt cur = prefetch_class<NT, BUF, FILL>(a, rsrc, next[0], cr, s_start, s_len, s_field, lane, v);
+        run_class<0, NT, BUF, FILL>(a, rsrc, cr, next[1], s_start, s_len, s_field, cls == 0, rank, lane, cur, v, mine);
+        run_class<1, NT, BUF, FILL>(a, rsrc, cr, next[2], s_start, s_len, s_field, cls == 1, rank, lane, cur, v, mine);
+        run_class<2, NT, BUF, FILL>(a, rsrc, cr, next[3], s_start, s_len, s_field, cls == 2, rank, lane, cur, v, mine);
+        run_class<3, NT, BUF, FILL>(a, rsrc, cr, next[4], s_start, s_len, s_field, cls == 3, rank, lane, cur, v, mine);
+        run_class<4, NT, BUF, FILL>(a, rsrc, cr, next[5], s_start, s_len, s_field, cls == 4, rank, lane, cur, v, mine);
 
         const uint16_t res = finalize(mine, d_start, d_len, d_seed, d_ok, a.flags);
-        if (live)
+        if (live && a.out)
             a.out[p] = res;  // 64 consecutive u16: one 128-byte store
+        if constexpr (FILL) {
+            if (live && d_ok) {  // set_be16(&mut header[f..f+2], checksum)
+                uint8_t *q = const_cast<uint8_t *>(a.arena) + own_start + d_field;
+                if ((reinterpret_cast<uintptr_t>(q) & 1) == 0) {
+                    *reinterpret_cast<uint16_t *>(q) = static_cast<uint16_t>((res >> 8) | (res << 8));
+                } else {
+                    q[0] = static_cast<uint8_t>(res >> 8);
+                    q[1] = static_cast<uint8_t>(res);
+                }
+            }
+        }
         if (a.bad) {
             const uint64_t rejected = __ballot(live && !d_ok);
             if (rejected && lane == 0)
                 atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fragment chains (util.rs:112-119 compute_buffer_ones_comp over NetBuffer
+// fragments, buf.rs:466-487).  Pass 1 is the packet kernel run over FRAGMENTS
+// with seed 0: frag_sums[f] = compute_ones_comp(0, fragment f), pairing bytes from
+// the fragment's own start exactly as the per-fragment call does.  Pass 2 (this
+// kernel) chains them: for fragments <= 128 KiB no step can wrap the u32, so the
+// reference's fold-after-every-fragment equals ONE end-around fold of
+// seed + sum(frag_sums) — both are the unique value in [1, 0xffff] congruent mod
+// 0xffff to seed + all words, or 0 when seed and every byte are 0.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void chain_combine_kernel(const uint64_t *__restrict__ frag_off,
+                                                               const uint32_t *__restrict__ frag_len,
+                                                               const uint16_t *__restrict__ frag_sums,
+                                                               uint32_t n_frags, const uint32_t *__restrict__ first,
+                                                               const uint16_t *__restrict__ seed,
+                                                               uint16_t *__restrict__ out, uint32_t n_pkts,
+                                                               uint64_t arena_bytes, uint32_t flags, uint32_t *bad)
+{
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_pkts; i += stride) {
+        const uint32_t f0 = first[i], f1 = first[i + 1];
+        bool ok = f0 <= f1 && f1 <= n_frags;
+        uint32_t acc = seed ? seed[i] : 0u;
+        for (uint32_t f = f0; ok && f < f1; ++f) {
+            const uint64_t o = frag_off[f];
+            const uint32_t L = frag_len[f];
+            ok = o <= arena_bytes && L <= arena_bytes - o;
+            acc += frag_sums[f];
+        }
+        while (acc > 0xffff)
+            acc = (acc & 0xffff) + (acc >> 16);
+        if (flags & RNS_FLAG_COMPLEMENT)
+            acc ^= 0xffff;
+        if (!ok) {
+            acc = 0;
+            if (bad)
+                atomicAdd(bad, 1u);
+        }
+        out[i] = static_cast<uint16_t>(acc);
     }
 }
 
@@ -700,13 +794,13 @@ int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipSt
     const bool buf = a.arena_bytes < kOobOffset;  // buffer loads need a 32-bit offset range
     if (variant & 4) {
         if (nt && buf)
-            hipLaunchKernelGGL((csum_mixed_kernel<S, true, true>), grid, block, 0, st, a);
+            hipLaunchKernelGGL((csum_mixed_kernel<S, true, true, false>), grid, block, 0, st, a);
         else if (nt)
-            hipLaunchKernelGGL((csum_mixed_kernel<S, true, false>), grid, block, 0, st, a);
+            hipLaunchKernelGGL((csum_mixed_kernel<S, true, false, false>), grid, block, 0, st, a);
         else if (buf)
-            hipLaunchKernelGGL((csum_mixed_kernel<S, false, true>), grid, block, 0, st, a);
+            hipLaunchKernelGGL((csum_mixed_kernel<S, false, true, false>), grid, block, 0, st, a);
         else
-            hipLaunchKernelGGL((csum_mixed_kernel<S, false, false>), grid, block, 0, st, a);
+            hipLaunchKernelGGL((csum_mixed_kernel<S, false, false, false>), grid, block, 0, st, a);
     } else if ((variant & 1) == 0) {
         if (nt)
             hipLaunchKernelGGL((csum_batch_kernel<G, U, S, true>), grid, block, 0, st, a);
@@ -902,6 +996,71 @@ int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uin
     a.flags = flags;
     const Shape sh = pick_shape(len);
     return dispatch<true>(a, sh.variant, sh.G, sh.U, sh.max_blocks, static_cast<hipStream_t>(stream));
+}
+
+int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_frag_off,
+                       const uint32_t *d_frag_len, uint32_t n_frags, const uint32_t *d_first,
+                       const uint16_t *d_seed, uint16_t *d_out, uint32_t n_pkts, uint32_t flags,
+                       uint32_t frag_len_hint, uint16_t *d_frag_sums, uint32_t *d_bad, void *stream)
+{
+    if (n_pkts == 0)
+        return RNS_OK;
+    if (!d_arena || !d_first || !d_out || (n_frags && (!d_frag_off || !d_frag_len || !d_frag_sums)))
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    // pass 1: every fragment as its own packet, seed 0, not complemented, no bad counting here
+    if (n_frags) {
+        const Shape sh = pick_shape(frag_len_hint ? frag_len_hint : 512u);
+        CsumArgs a{};
+        set_arena(a, d_arena, arena_bytes);
+        a.off = d_frag_off;
+        a.len = d_frag_len;
+        a.seed = nullptr;
+        a.out = d_frag_sums;
+        a.bad = nullptr;
+        a.n = n_frags;
+        a.flags = 0;
+        if (int st = dispatch<false>(a, sh.variant, sh.G, sh.U, sh.max_blocks, static_cast<hipStream_t>(stream)))
+            return st;
+    }
+    // pass 2: chain per packet
+    const uint32_t blocks = static_cast<uint32_t>(std::min<uint64_t>((n_pkts + kBlock - 1) / kBlock, 4096));
+    hipLaunchKernelGGL(chain_combine_kernel, dim3(blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                       d_frag_off, d_frag_len, d_frag_sums, n_frags, d_first, d_seed, d_out, n_pkts, arena_bytes,
+                       flags, d_bad);
+    return hip_status(hipGetLastError());
+}
+
+int rns_csum_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off, const uint32_t *d_len,
+                      const uint16_t *d_seed, const uint16_t *d_field, uint32_t field_off, uint16_t *d_out,
+                      uint32_t n, uint32_t flags, uint32_t *d_bad, void *stream)
+{
+    if (n == 0)
+        return RNS_OK;
+    if (!d_arena || !d_off || !d_len)
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    CsumArgs a{};
+    set_arena(a, d_arena, arena_bytes);
+    a.off = d_off;
+    a.len = d_len;
+    a.seed = d_seed;
+    a.out = d_out;
+    a.bad = d_bad;
+    a.n = n;
+    a.flags = flags;
+    a.field = d_field;
+    a.field_off = field_off;
+    const uint64_t blocks = ((static_cast<uint64_t>(n) + 63) / 64 + kBlock / 64 - 1) / (kBlock / 64);
+    const dim3 grid(static_cast<uint32_t>(blocks)), block(kBlock);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (a.arena_bytes < kOobOffset)
+        hipLaunchKernelGGL((csum_mixed_kernel<false, false, true, true>), grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL((csum_mixed_kernel<false, false, false, true>), grid, block, 0, st, a);
+    return hip_status(hipGetLastError());
 }
 
 int rns_host_ctx_create(int device, uint64_t chunk_bytes, uint32_t nstreams, rns_host_ctx **out)

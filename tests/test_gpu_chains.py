@@ -1,0 +1,96 @@
+"""GPU fragment chains (rns_csum_chain_dev): util.rs:112-119 compute_buffer_ones_comp
+over NetBuffer-style fragment lists, bit-exact against the oracle."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import sweep_arena
+from oracle import oracle as O
+from rustnetworkstack_amd.batch import csum_batch, csum_chain
+from rustnetworkstack_amd.workloads import DeviceBatch, make_layout
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def dev(a, view):
+    return torch.from_numpy(np.ascontiguousarray(a).view(view)).to(DEV)
+
+
+def host_u16(t):
+    torch.cuda.synchronize()
+    return t.view(torch.int16).cpu().numpy().view(np.uint16)
+
+
+def run_chain(arena_t, offs, lens, first, seeds, complement=False, bad=None):
+    return host_u16(csum_chain(arena_t, dev(np.asarray(offs, dtype=np.uint64), np.int64),
+                               dev(np.asarray(lens, dtype=np.uint32), np.int32),
+                               dev(np.asarray(first, dtype=np.uint32), np.int32),
+                               None if seeds is None else dev(np.asarray(seeds, dtype=np.uint16), np.int16),
+                               complement=complement, bad=bad))
+
+
+def test_reference_kats():
+    # util.rs:303-312: two 512-byte fragments of 12 34 -> 0x6824; odd non-final fragment -> 0x0807
+    buf = np.frombuffer(bytes([0x12, 0x34]) * 512 + bytes([1, 2, 3, 0, 4, 5]), dtype=np.uint8).copy()
+    a = torch.from_numpy(buf).to(DEV)
+    got = run_chain(a, [0, 512, 1024, 1028], [512, 512, 3, 2], [0, 2, 4], [0, 0])
+    assert list(got) == [0x6824, 0x0807]
+
+
+def test_golden_fixture_chains(sweep):
+    arena = torch.from_numpy(sweep_arena(sweep)).to(DEV)
+    offs, lens, first, seeds = [], [], [0], []
+    for ch in sweep["chains"]:
+        for o, s in ch["frags"]:
+            offs.append(o)
+            lens.append(s)
+        first.append(len(offs))
+        seeds.append(ch["seed"])
+    got = run_chain(arena, offs, lens, first, seeds)
+    assert np.array_equal(got, np.array([c["expect"] for c in sweep["chains"]], dtype=np.uint16))
+
+
+def test_random_scattered_chains(oracle):
+    """200K chains of 1-8 fragments of 1-700 B (odd sizes, scattered, any alignment)."""
+    n = 200_000
+    arena_np = O.splitmix64_bytes(0xC4A1, 64 << 20)
+    w = O.splitmix64_words(0xC4A2, n)
+    nfr = (w % np.uint64(8) + np.uint64(1)).astype(np.int64)
+    first = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(nfr, out=first[1:])
+    nf = int(first[-1])
+    fw = O.splitmix64_words(0xC4A3, nf)
+    lens = (fw % np.uint64(700) + np.uint64(1)).astype(np.uint32)
+    offs = ((fw >> np.uint64(20)) % np.uint64((64 << 20) - 1024)).astype(np.uint64)
+    seeds = (w >> np.uint64(40) & np.uint64(0xFFFF)).astype(np.uint16)
+    expect = oracle.chain_batch(arena_np, offs, lens, first, seeds, complement=True)
+    got = run_chain(torch.from_numpy(arena_np).to(DEV), offs, lens, first, seeds, complement=True)
+    assert np.array_equal(got, expect)
+
+
+def test_full_size_received_fragments_match_contiguous(oracle):
+    """Headline batch (1M x 1500 B) as the stack receives it after the IP trim
+    ([492, 512, 476]-byte fragments): chain result == contiguous result == oracle."""
+    lay = make_layout("c3_1500B")
+    b = DeviceBatch(lay, DEV)
+    contiguous = host_u16(csum_batch(b.arena, b.off, b.length, b.seed, complement=True))
+    sizes = np.array([492, 512, 496], dtype=np.uint32)
+    offs = (lay.off[:, None] + np.array([0, 492, 1004], dtype=np.uint64)[None, :]).reshape(-1)
+    lens = np.tile(sizes, lay.n)
+    first = np.arange(0, 3 * lay.n + 1, 3, dtype=np.uint32)
+    got = run_chain(b.arena, offs, lens, first, lay.seed, complement=True)
+    assert np.array_equal(got, contiguous)
+    sample = slice(0, 20000)
+    arena_np = b.arena[:int(lay.off[20000])].cpu().numpy()
+    expect = oracle.chain_batch(arena_np, offs[:60000], lens[:60000], first[:20001], lay.seed[sample], complement=True)
+    assert np.array_equal(got[sample], expect)
+    del b
+    torch.cuda.empty_cache()
+
+
+def test_bad_fragment_rejects_packet():
+    a = torch.zeros(4096, dtype=torch.uint8, device=DEV)
+    bad = torch.zeros(1, dtype=torch.int32, device=DEV)
+    got = run_chain(a, [0, 4000, 10], [16, 200, 4], [0, 2, 3], [5, 6], bad=bad)
+    assert got[0] == 0 and got[1] == 6 and int(bad.item()) == 1

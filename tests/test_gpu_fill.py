@@ -1,0 +1,120 @@
+"""Transmit in-place fill (rns_csum_fill_dev): tcp.rs:957-973, udp.rs:158-171,
+icmp.rs:87-112, ip.rs:158-159 — checksum computed with the field zeroed, stored
+big-endian into the field — bit-exact against the oracle, and every filled packet
+passes the receive check (tcp.rs:838-850 / ip.rs:76-80) afterwards."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from rustnetworkstack_amd.batch import csum_batch, csum_fill
+from rustnetworkstack_amd.workloads import DeviceBatch, make_layout
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def dev(a, view):
+    return torch.from_numpy(np.ascontiguousarray(a).view(view)).to(DEV)
+
+
+def host_u16(t):
+    torch.cuda.synchronize()
+    return t.view(torch.int16).cpu().numpy().view(np.uint16)
+
+
+def expected_fill(oracle, arena_np, off, ln, seeds, field):
+    """Reference: zero the field (alloc_header), compute 0xffff ^ ones_comp(seed, packet)."""
+    a = arena_np.copy()
+    for o, f in zip(off, field):
+        a[int(o) + int(f)] = 0
+        a[int(o) + int(f) + 1] = 0
+    return a, oracle.batch(a, off, ln, seeds, complement=True)
+
+
+def stored_be(arena_np, off, field):
+    idx = off.astype(np.int64) + field.astype(np.int64)
+    return (arena_np[idx].astype(np.uint16) << 8) | arena_np[idx + 1].astype(np.uint16)
+
+
+def test_full_size_tcp_fill_then_receive_verify(oracle):
+    """Headline batch: fill TCP checksums ([16..18]) of 1M x 1500 B segments with
+    per-packet pseudo-header seeds; stored values == oracle; receive check == 0 for all."""
+    lay = make_layout("c3_1500B")
+    b = DeviceBatch(lay, DEV)
+    out = torch.empty(lay.n, dtype=torch.uint16, device=DEV)
+    csum_fill(b.arena, b.off, b.length, b.seed, field_off=16, out=out)
+    rx = csum_batch(b.arena, b.off, b.length, b.seed, complement=True)
+    assert int((rx.view(torch.int16) != 0).sum().item()) == 0
+    k = 30000
+    end = int(lay.off[k])
+    filled = b.arena[:end].cpu().numpy()
+    field = np.full(k, 16, dtype=np.uint32)
+    # the oracle does not care what the field held before: it zeroes it first
+    _, expect = expected_fill(oracle, filled, lay.off[:k], lay.length[:k], lay.seed[:k], field)
+    assert np.array_equal(stored_be(filled, lay.off[:k], field), expect)
+    assert np.array_equal(host_u16(out)[:k], expect)
+    del b
+    torch.cuda.empty_cache()
+
+
+def test_mixed_fields_any_alignment(oracle):
+    """IMIX packets at odd and even offsets, per-packet field offsets 2 / 6 / 10 / 16
+    (ICMP / UDP / IPv4 / TCP) at any parity, arbitrary prior field contents."""
+    n = 50000
+    lay = make_layout("c5_imix", n=n)
+    w = O.splitmix64_words(0xF1E1D, n)
+    shift = (w & np.uint64(7)).astype(np.uint64)                     # odd and even starts
+    off = lay.off + shift
+    ln = np.maximum(lay.length - 8, 20).astype(np.uint32)
+    field = np.array([2, 6, 10, 16, 3, 17], dtype=np.uint32)[(w >> np.uint64(8)) % np.uint64(6)]
+    arena_np = O.splitmix64_bytes(0xABBA, lay.arena_bytes + 16)
+    _, expect = expected_fill(oracle, arena_np, off, ln, lay.seed, field)
+    arena = torch.from_numpy(arena_np.copy()).to(DEV)
+    out = torch.empty(n, dtype=torch.uint16, device=DEV)
+    csum_fill(arena, dev(off, np.int64), dev(ln, np.int32), dev(lay.seed, np.int16),
+              field=dev(field.astype(np.uint16), np.int16), out=out)
+    got_arena = arena.cpu().numpy()
+    assert np.array_equal(host_u16(out), expect)
+    assert np.array_equal(stored_be(got_arena, off, field), expect)
+    # nothing outside the fields changed
+    mask = np.ones(got_arena.shape[0], dtype=bool)
+    idx = off.astype(np.int64) + field.astype(np.int64)
+    mask[idx] = False
+    mask[idx + 1] = False
+    assert np.array_equal(got_arena[mask], arena_np[mask])
+
+
+def test_ipv4_header_fill():
+    """ip.rs:158-159: checksum over the 20-byte header stored at [10..12]; the
+    receive check (ip.rs:76, compute_checksum == 0) then passes."""
+    hdr = bytes.fromhex("450000730000400040110000c0a80001c0a800c7")   # textbook header, checksum 0xb861
+    arena = torch.from_numpy(np.frombuffer(hdr * 1000, dtype=np.uint8).copy()).to(DEV)
+    off = dev(np.arange(1000, dtype=np.uint64) * np.uint64(20), np.int64)
+    ln = dev(np.full(1000, 20, dtype=np.uint32), np.int32)
+    csum_fill(arena, off, ln, None, field_off=10)
+    a = arena.cpu().numpy().reshape(1000, 20)
+    assert np.all(a[:, 10] == 0xB8) and np.all(a[:, 11] == 0x61)
+    assert int((csum_batch(arena, off, ln, complement=True).view(torch.int16) != 0).sum()) == 0
+
+
+def test_udp_zero_checksum_stored_as_is():
+    """udp.rs:168-171 stores the computed value even when it is 0 (no RFC 768 0 -> 0xffff)."""
+    pkt = np.array([0xFF, 0xFF, 0, 0, 0, 0, 0x12, 0x34], dtype=np.uint8)   # field [6..8] holds junk
+    arena = torch.from_numpy(pkt.copy()).to(DEV)
+    out = torch.empty(1, dtype=torch.uint16, device=DEV)
+    csum_fill(arena, dev(np.array([0], dtype=np.uint64), np.int64), dev(np.array([8], dtype=np.uint32), np.int32),
+              None, field_off=6, out=out)
+    assert list(arena.cpu().numpy()[6:8]) == [0, 0] and host_u16(out)[0] == 0
+
+
+def test_field_out_of_packet_is_rejected():
+    arena = torch.arange(64, dtype=torch.uint8, device=DEV)
+    before = arena.cpu().numpy().copy()
+    bad = torch.zeros(1, dtype=torch.int32, device=DEV)
+    out = torch.empty(2, dtype=torch.uint16, device=DEV)
+    csum_fill(arena, dev(np.array([0, 40], dtype=np.uint64), np.int64),
+              dev(np.array([17, 30], dtype=np.uint32), np.int32), None, field_off=16, out=out, bad=bad)
+    assert int(bad.item()) == 2          # 16+2 > 17, and 40+30 > 64
+    assert np.array_equal(arena.cpu().numpy(), before)
+    assert list(host_u16(out)) == [0, 0]

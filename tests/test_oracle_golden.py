@@ -96,3 +96,17 @@ def test_batch_mt_equals_single(oracle):
 def test_splitmix64_known_value():
     # splitmix64 with state 0: first output 0xe220a8397b1dcdaf (Vigna's reference generator)
     assert int(O.splitmix64_words(0, 1)[0]) == 0xE220A8397B1DCDAF
+
+
+def test_chain_batch_matches_per_packet_chains(oracle, sweep):
+    """The C batch-of-chains restatement agrees with the single-chain one on the fixtures."""
+    arena = sweep_arena(sweep)
+    offs, lens, first, seeds = [], [], [0], []
+    for ch in sweep["chains"]:
+        for o, s in ch["frags"]:
+            offs.append(o)
+            lens.append(s)
+        first.append(len(offs))
+        seeds.append(ch["seed"])
+    got = oracle.chain_batch(arena, np.array(offs), np.array(lens), np.array(first), np.array(seeds))
+    assert np.array_equal(got, np.array([ch["expect"] for ch in sweep["chains"]], dtype=np.uint16))
