@@ -231,6 +231,12 @@ constexpr uint32_t kNoWrapBytes = 131072;
 // after the compiler folds an immediate offset (<= 4095) into it.
 constexpr uint32_t kOobOffset = 0xFFFFF000u;
 
+// Buffer range checks are per dword: a dword that straddles num_records reads as
+// zero.  The descriptor therefore covers the arena rounded up to whole 16-byte
+// chunks (the bytes past arena_bytes share a chunk, hence a page, with valid
+// bytes, and are masked away like every byte outside a packet).
+__host__ __device__ __forceinline__ uint64_t buf_records(const CsumArgs &a) { return (a.arena_bytes + 15) & ~15ull; }
+
 struct Pkt {
     uint64_t start;       // packet byte offset from the 16-byte aligned arena base
     uint32_t nch;         // 16-byte chunks covering the packet (0 if empty)
@@ -424,7 +430,7 @@ __global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
     const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
     // Whole-arena buffer descriptor (used only when BUF: the arena fits a 32-bit offset).
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? a.arena_bytes : 0), 0x00020000);
+        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
 
     for (uint64_t base = static_cast<uint64_t>(wave) * 64; base < a.n; base += static_cast<uint64_t>(nwaves) * 64) {
         const uint64_t p = base + lane;
@@ -614,7 +620,7 @@ __global__ __launch_bounds__(kBlock, (BUF && !FILL) ? 4 : 3) void csum_mixed_ker
     const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? a.arena_bytes : 0), 0x00020000);
+        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
 
     for (uint64_t base = static_cast<uint64_t>(wave) * 64; base < a.n; base += static_cast<uint64_t>(nwaves) * 64) {
         const uint64_t p = base + lane;
@@ -791,7 +797,7 @@ int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipSt
         return RNS_OK;
     const dim3 grid(static_cast<uint32_t>(blocks)), block(kBlock);
     const bool nt = (variant & 2) != 0;
-    const bool buf = a.arena_bytes < kOobOffset;  // buffer loads need a 32-bit offset range
+    const bool buf = buf_records(a) < kOobOffset;  // buffer loads need a 32-bit offset range
     if (variant & 4) {
         if (nt && buf)
             hipLaunchKernelGGL((csum_mixed_kernel<S, true, true, false>), grid, block, 0, st, a);
@@ -1056,7 +1062,7 @@ int rns_csum_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_
     const uint64_t blocks = ((static_cast<uint64_t>(n) + 63) / 64 + kBlock / 64 - 1) / (kBlock / 64);
     const dim3 grid(static_cast<uint32_t>(blocks)), block(kBlock);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (a.arena_bytes < kOobOffset)
+    if (buf_records(a) < kOobOffset)
         hipLaunchKernelGGL((csum_mixed_kernel<false, false, true, true>), grid, block, 0, st, a);
     else
         hipLaunchKernelGGL((csum_mixed_kernel<false, false, false, true>), grid, block, 0, st, a);

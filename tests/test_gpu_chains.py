@@ -89,6 +89,15 @@ def test_full_size_received_fragments_match_contiguous(oracle):
     torch.cuda.empty_cache()
 
 
+def test_chain_tail_at_unpadded_arena_end(oracle):
+    """Fragments ending on the last byte of an arena whose size is not a multiple of 4."""
+    arena_np = O.splitmix64_bytes(3, 1030)
+    got = run_chain(torch.from_numpy(arena_np.copy()).to(DEV), [0, 1024, 1028], [1024, 3, 2], [0, 1, 3], [7, 9])
+    expect = oracle.chain_batch(arena_np, np.array([0, 1024, 1028]), np.array([1024, 3, 2]), np.array([0, 1, 3]),
+                                np.array([7, 9], dtype=np.uint16))
+    assert np.array_equal(got, expect)
+
+
 def test_bad_fragment_rejects_packet():
     a = torch.zeros(4096, dtype=torch.uint8, device=DEV)
     bad = torch.zeros(1, dtype=torch.int32, device=DEV)

@@ -242,3 +242,18 @@ def test_arena_beyond_4gib_uses_64bit_path(oracle):
         assert np.array_equal(host_u16(csum_batch(arena, *d, shape=shape)), expect), shape
     del arena
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("total", [4093, 4094, 4095, 4097, 4101, 4111])
+def test_packets_ending_at_unpadded_arena_end(oracle, total):
+    """Arena lengths that are not a multiple of 4 or 16, packets ending exactly at the
+    last byte, at every start parity: no kernel may drop the tail bytes."""
+    arena_np = O.splitmix64_bytes(total, total)
+    arena = torch.from_numpy(arena_np.copy()).to(DEV)
+    lens = np.array([1, 2, 3, 5, 7, 16, 17, 40, 64, 333, 1500], dtype=np.uint32)
+    off = (total - lens).astype(np.uint64)
+    sd = np.arange(len(lens), dtype=np.uint16) * np.uint16(4099)
+    expect = oracle.batch(arena_np, off, lens, sd)
+    d = dev_desc(off, lens, sd)
+    for shape in [None] + [(v, g, u, 0) for v in range(8) for g, u in ((4, 1), (16, 4), (64, 2))]:
+        assert np.array_equal(host_u16(csum_batch(arena, *d, shape=shape)), expect), shape
