@@ -78,6 +78,70 @@ def pseudo_header_py(src: bytes, dst: bytes, length: int, protocol: int) -> int:
     return ones_comp_py(0, bytes(ph))
 
 
+# receive path restated (status bits of include/rns_checksum.h RNS_RX_*)
+RX_IP_OK, RX_L4_OK, RX_L4_UNCHECKED, RX_FRAGMENT, RX_UNKNOWN, RX_ACCEPT, RX_MALFORMED = (
+    0x01, 0x02, 0x04, 0x08, 0x10, 0x40, 0x80)
+
+
+def rx_status_ref(pkt: bytes, local4: bytes, local6: bytes, ones_comp=None) -> int:
+    """What the reference's receive path decides for one datagram, as status bits.
+
+    ip_input (ip.rs:38-48) -> ip_input_v4 (ip.rs:65-92: header checksum over
+    header[..IHL*4], fragment drop, protocol header[9], source header[12..16],
+    trim_head(IHL*4)) / ip_input_v6 (ip.rs:108-115: protocol header[6], source
+    header[8..24], trim_head(40)) -> ip_input_common (ip.rs:117-128) -> tcp_input's
+    validate_checksum (tcp.rs:838-850: pseudo-header with dest = local address of
+    the source's family, length = remaining buffer length), icmp_input_v4
+    (icmp.rs:44-50: no pseudo-header), icmp_input_v6 (icmp.rs:62-75: dest = local
+    IPv6), udp_input (udp.rs:126-148: no check).  Where the Rust code would panic
+    (empty header slice, short buffers, trim past the end, V4 source in a V6
+    pseudo-header) or rejects the version, the result is RX_MALFORMED.
+    """
+    oc = ones_comp or ones_comp_py
+    L = len(pkt)
+    if L == 0:
+        return RX_MALFORMED
+    version = pkt[0] >> 4
+    if version == 4:
+        hdr = (pkt[0] & 0xF) * 4
+        if hdr == 0 or L < 16 or hdr > L:
+            return RX_MALFORMED
+        st = RX_IP_OK if (0xFFFF ^ oc(0, pkt[:hdr])) == 0 else 0
+        if ((pkt[6] << 8 | pkt[7]) & 0x3FFF) != 0:
+            st |= RX_FRAGMENT
+        proto, src = pkt[9], pkt[12:16]
+    elif version == 6:
+        hdr = 40
+        if L < 40:
+            return RX_MALFORMED
+        st = RX_IP_OK
+        proto, src = pkt[6], pkt[8:24]
+    else:
+        return RX_MALFORMED
+    seg = pkt[hdr:]
+
+    def buf_sum(seed):  # compute_buffer_ones_comp over a one-fragment buffer; empty buffer -> seed
+        return oc(seed, seg) if len(seg) else seed
+
+    if proto == 6:
+        dst = local4 if len(src) == 4 else local6
+        ok = (buf_sum(pseudo_header_py(src, dst, len(seg), 6)) ^ 0xFFFF) == 0
+        st |= RX_L4_OK if ok else 0
+    elif proto == 1:
+        st |= RX_L4_OK if (buf_sum(0) ^ 0xFFFF) == 0 else 0
+    elif proto == 58:
+        if len(src) == 4:
+            return RX_MALFORMED
+        st |= RX_L4_OK if (buf_sum(pseudo_header_py(src, local6, len(seg), 58)) ^ 0xFFFF) == 0 else 0
+    elif proto == 17:
+        st |= RX_L4_UNCHECKED
+    else:
+        st |= RX_UNKNOWN
+    if (st & RX_IP_OK) and not (st & RX_FRAGMENT) and (st & (RX_L4_OK | RX_L4_UNCHECKED)):
+        st |= RX_ACCEPT
+    return st
+
+
 # --------------------------------------------------------------------------
 # deterministic synthetic bytes: splitmix64 (SURVEY §8d, seed 0x5EED_C0DE)
 # --------------------------------------------------------------------------

@@ -22,6 +22,13 @@ RNS_E_ORDER = -5
 RNS_E_TOOLARGE = -6
 RNS_E_HIP_BASE = -1000
 RNS_FLAG_COMPLEMENT = 0x1
+RNS_RX_IP_OK = 0x01
+RNS_RX_L4_OK = 0x02
+RNS_RX_L4_UNCHECKED = 0x04
+RNS_RX_FRAGMENT = 0x08
+RNS_RX_UNKNOWN_PROTO = 0x10
+RNS_RX_ACCEPT = 0x40
+RNS_RX_MALFORMED = 0x80
 
 # Every symbol include/rns_checksum.h declares (tests/test_abi.py checks the header,
 # this list and the library's dynamic symbol table agree).
@@ -35,6 +42,8 @@ EXPORTED_SYMBOLS = (
     "rns_csum_batch_dev_cfg",
     "rns_csum_chain_dev",
     "rns_csum_fill_dev",
+    "rns_rx_verify_workspace_bytes",
+    "rns_rx_verify_dev",
     "rns_host_ctx_create",
     "rns_host_ctx_destroy",
     "rns_csum_batch_host",
@@ -86,6 +95,8 @@ _SIGNATURES = {
     "rns_csum_batch_dev_cfg": (_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _u32, _vp, _vp]),
     "rns_csum_chain_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp]),
     "rns_csum_fill_dev": (_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u32, _vp, _u32, _u32, _vp, _vp]),
+    "rns_rx_verify_workspace_bytes": (_u64, [_u32]),
+    "rns_rx_verify_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
     "rns_host_ctx_create": (_int, [_int, _u64, _u32, ctypes.POINTER(_vp)]),
     "rns_host_ctx_destroy": (_int, [_vp]),
     "rns_csum_batch_host": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32]),

@@ -226,6 +226,36 @@ def csum_fill(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, seed
     return out
 
 
+def rx_verify(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, local_ipv4: bytes, local_ipv6: bytes,
+              *, status: torch.Tensor | None = None, l4_sum: torch.Tensor | None = None,
+              workspace: torch.Tensor | None = None) -> torch.Tensor:
+    """Receive verify of a batch of IP datagrams (rns_rx_verify_dev): returns a uint8
+    status per packet (RNS_RX_* bits; RNS_RX_ACCEPT = the stack would deliver it)."""
+    _require_cuda(arena, "arena", (torch.uint8,))
+    _require_cuda(off, "off", (torch.int64,))
+    _require_cuda(length, "length", (torch.int32,))
+    if len(local_ipv4) != 4 or len(local_ipv6) != 16:
+        raise ValueError("local_ipv4 must be 4 bytes and local_ipv6 16 bytes")
+    n = off.numel()
+    dev = arena.device
+    lib = _lib.load()
+    need = int(lib.rns_rx_verify_workspace_bytes(n))
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+    if status is None:
+        status = torch.empty(n, dtype=torch.uint8, device=dev)
+    l4_ptr = None
+    if l4_sum is not None:
+        _require_cuda(l4_sum, "l4_sum", _U16)
+        l4_ptr = l4_sum.data_ptr()
+    with torch.cuda.device(dev):
+        st = lib.rns_rx_verify_dev(arena.data_ptr(), arena.numel(), off.data_ptr(), length.data_ptr(), n,
+                                   bytes(local_ipv4), bytes(local_ipv6), status.data_ptr(), l4_ptr,
+                                   workspace.data_ptr(), workspace.numel(), _stream_handle(dev))
+    _lib.check(st, "rns_rx_verify_dev")
+    return status
+
+
 def fill_splitmix64(buf: torch.Tensor, seed: int) -> torch.Tensor:
     """Fill a device uint8 buffer with the splitmix64 byte stream (same bytes as
     oracle.splitmix64_bytes(seed, n))."""

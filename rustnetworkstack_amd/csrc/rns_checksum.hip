@@ -759,6 +759,160 @@ __global__ __launch_bounds__(kBlock) void chain_combine_kernel(const uint64_t *_
     }
 }
 
+// ---------------------------------------------------------------------------
+// Receive verify (§8f row 1): the checks ip_input_v4 (ip.rs:65-92), ip_input_v6
+// (ip.rs:108-115), ip_input_common (ip.rs:117-128), tcp::validate_checksum
+// (tcp.rs:838-850), icmp_input_v4 (icmp.rs:44-50) and icmp_input_v6 (icmp.rs:62-75)
+// apply to a received datagram, for a whole batch:
+//   1. rx_parse_kernel (thread per packet) reads the few header bytes it needs,
+//      forms the pseudo-header sum (util.rs:180-207, dest = the LOCAL address as
+//      the reference passes netif::get_ipaddr()) and emits two byte ranges per
+//      packet: the IPv4 header, and the L4 segment seeded with that sum;
+//   2. the mixed checksum kernel sums the 2n ranges (complemented) in one pass
+//      over the packet bytes (UDP / unknown protocols: the L4 range is empty,
+//      the stack never verifies them, udp.rs:126-148);
+//   3. rx_verdict_kernel turns sums + parse flags into a status byte.
+// ---------------------------------------------------------------------------
+enum : uint8_t {
+    kMetaV4 = 1, kMetaV6 = 2, kMetaFrag = 4, kMetaMalformed = 8,
+    kMetaL4Checked = 16, kMetaUnchecked = 32, kMetaUnknown = 64,
+};
+
+struct RxArgs {
+    const uint8_t *arena;  // caller's base (any alignment; byte loads)
+    uint64_t arena_bytes;
+    const uint64_t *off;
+    const uint32_t *len;
+    uint32_t n;
+    uint32_t local4_sum;   // BE word sum of the local IPv4 address
+    uint32_t local6_sum;   // BE word sum of the local IPv6 address
+    uint64_t *r_off;       // 2n ranges
+    uint32_t *r_len;
+    uint16_t *r_seed;
+    uint8_t *meta;
+};
+
+__device__ __forceinline__ uint32_t fold16(uint32_t x)
+{
+    while (x > 0xffff)
+        x = (x & 0xffff) + (x >> 16);
+    return x;
+}
+
+__global__ __launch_bounds__(kBlock) void rx_parse_kernel(const RxArgs a)
+{
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+        const uint64_t o = a.off[i];
+        const uint32_t L = a.len[i];
+        uint8_t meta = 0;
+        uint32_t hdr = 0, ph = 0;
+        bool l4_read = false;
+        const bool inb = o <= a.arena_bytes && L <= a.arena_bytes - o;
+        if (!inb || L == 0) {
+            meta = kMetaMalformed;
+        } else {
+            const uint8_t *p = a.arena + o;
+            const uint32_t version = p[0] >> 4;                    // ip.rs:40
+            uint32_t proto = 0, src_sum = 0;
+            bool v4src = false;
+            if (version == 4) {
+                hdr = (p[0] & 0xf) * 4u;                           // ip.rs:71
+                if (hdr == 0 || L < 16 || hdr > L) {               // empty slice / header index / trim_head panic
+                    meta = kMetaMalformed;
+                } else {
+                    meta = kMetaV4;
+                    if (((static_cast<uint32_t>(p[6]) << 8 | p[7]) & 0x3fff) != 0)  // ip.rs:84-87
+                        meta |= kMetaFrag;
+                    proto = p[9];                                  // ip.rs:89
+                    src_sum = (static_cast<uint32_t>(p[12]) << 8 | p[13]) + (static_cast<uint32_t>(p[14]) << 8 | p[15]);
+                    v4src = true;
+                }
+            } else if (version == 6) {
+                hdr = 40;
+                if (L < 40) {                                      // trim_head(IPV6_HEADER_LEN) would panic
+                    meta = kMetaMalformed;
+                } else {
+                    meta = kMetaV6;
+                    proto = p[6];                                  // ip.rs:110
+                    for (int k = 8; k < 24; k += 2)                // source address ip.rs:111
+                        src_sum += static_cast<uint32_t>(p[k]) << 8 | p[k + 1];
+                }
+            } else {
+                meta = kMetaMalformed;                             // "IP: Invalid version field"
+            }
+            if (!(meta & kMetaMalformed)) {
+                const uint32_t l4len = L - hdr;                    // packet.len() after trim_head
+                if (proto == 6) {                                  // tcp.rs:838-850: dest = local address of src's family
+                    ph = v4src ? fold16(src_sum + a.local4_sum + 6 + (l4len & 0xffff))
+                               : fold16(src_sum + a.local6_sum + (l4len >> 16) + (l4len & 0xffff) + 6);
+                    meta |= kMetaL4Checked;
+                    l4_read = true;
+                } else if (proto == 1) {                           // icmp.rs:46: no pseudo header
+                    ph = 0;
+                    meta |= kMetaL4Checked;
+                    l4_read = true;
+                } else if (proto == 58) {                          // icmp.rs:63-68: dest = local IPv6
+                    if (v4src) {
+                        meta |= kMetaMalformed;                    // V4 source into a V6 pseudo-header: copy_to panics
+                    } else {
+                        ph = fold16(src_sum + a.local6_sum + (l4len >> 16) + (l4len & 0xffff) + 58);
+                        meta |= kMetaL4Checked;
+                        l4_read = true;
+                    }
+                } else if (proto == 17) {
+                    meta |= kMetaUnchecked;                        // udp.rs:126-148 never verifies
+                } else {
+                    meta |= kMetaUnknown;                          // ip.rs:126 "Unknown protocol"
+                }
+            }
+        }
+        // range 2i: the IPv4 header (checksum over header[..IHL*4], ip.rs:76); an empty
+        // range seeded 0xffff for IPv6 / malformed (complemented result 0: nothing to check)
+        const bool v4 = (meta & kMetaV4) && !(meta & kMetaMalformed);
+        a.r_off[2 * i] = inb ? o : 0;
+        a.r_len[2 * i] = v4 ? hdr : 0u;
+        a.r_seed[2 * i] = v4 ? 0 : 0xffff;
+        // range 2i+1: the L4 segment seeded with the pseudo-header sum
+        const bool l4 = l4_read && !(meta & kMetaMalformed);
+        a.r_off[2 * i + 1] = l4 ? o + hdr : 0;
+        a.r_len[2 * i + 1] = l4 ? L - hdr : 0u;
+        a.r_seed[2 * i + 1] = l4 ? static_cast<uint16_t>(ph) : static_cast<uint16_t>(0xffff);
+        a.meta[i] = meta;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void rx_verdict_kernel(const uint8_t *__restrict__ meta,
+                                                            const uint16_t *__restrict__ sums, uint32_t n,
+                                                            uint8_t *__restrict__ status,
+                                                            uint16_t *__restrict__ l4_out)
+{
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint8_t m = meta[i];
+        uint8_t st = 0;
+        if (m & kMetaMalformed) {
+            st = RNS_RX_MALFORMED;
+        } else {
+            if ((m & kMetaV6) || sums[2 * i] == 0)       // compute_checksum(header) == 0 (ip.rs:76-80)
+                st |= RNS_RX_IP_OK;
+            if (m & kMetaFrag)
+                st |= RNS_RX_FRAGMENT;
+            if ((m & kMetaL4Checked) && sums[2 * i + 1] == 0)  // buffer sum ^ 0xffff == 0
+                st |= RNS_RX_L4_OK;
+            if (m & kMetaUnchecked)
+                st |= RNS_RX_L4_UNCHECKED;
+            if (m & kMetaUnknown)
+                st |= RNS_RX_UNKNOWN_PROTO;
+            if ((st & RNS_RX_IP_OK) && !(st & RNS_RX_FRAGMENT) && (st & (RNS_RX_L4_OK | RNS_RX_L4_UNCHECKED)))
+                st |= RNS_RX_ACCEPT;
+        }
+        status[i] = st;
+        if (l4_out)
+            l4_out[i] = sums[2 * i + 1];
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void splitmix64_fill_kernel(uint8_t *buf, uint64_t nbytes, uint64_t seed)
 {
     const uint64_t nwords = (nbytes + 7) / 8;
@@ -1066,6 +1220,72 @@ int rns_csum_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_
         hipLaunchKernelGGL((csum_mixed_kernel<false, false, true, true>), grid, block, 0, st, a);
     else
         hipLaunchKernelGGL((csum_mixed_kernel<false, false, false, true>), grid, block, 0, st, a);
+    return hip_status(hipGetLastError());
+}
+
+static uint64_t align_up(uint64_t x) { return (x + 255) & ~255ull; }
+
+uint64_t rns_rx_verify_workspace_bytes(uint32_t n)
+{
+    const uint64_t m = 2ull * n;
+    return align_up(m * 8) + align_up(m * 4) + align_up(m * 2) + align_up(m * 2) + align_up(n);
+}
+
+static uint32_t be_sum(const uint8_t *p, int nbytes)
+{
+    uint32_t s = 0;
+    for (int k = 0; k < nbytes; k += 2)
+        s += static_cast<uint32_t>(p[k]) << 8 | p[k + 1];
+    return s;
+}
+
+int rns_rx_verify_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off, const uint32_t *d_len,
+                      uint32_t n, const uint8_t *local_ipv4, const uint8_t *local_ipv6, uint8_t *d_status,
+                      uint16_t *d_l4_sum, void *d_workspace, uint64_t workspace_bytes, void *stream)
+{
+    if (n == 0)
+        return RNS_OK;
+    if (!d_arena || !d_off || !d_len || !d_status || !local_ipv4 || !local_ipv6 || !d_workspace)
+        return RNS_E_INVALID;
+    if (workspace_bytes < rns_rx_verify_workspace_bytes(n))
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint64_t m = 2ull * n;
+    uint8_t *w = static_cast<uint8_t *>(d_workspace);
+    RxArgs ra{};
+    ra.arena = d_arena;
+    ra.arena_bytes = arena_bytes;
+    ra.off = d_off;
+    ra.len = d_len;
+    ra.n = n;
+    ra.local4_sum = be_sum(local_ipv4, 4);
+    ra.local6_sum = be_sum(local_ipv6, 16);
+    ra.r_off = reinterpret_cast<uint64_t *>(w);
+    w += align_up(m * 8);
+    ra.r_len = reinterpret_cast<uint32_t *>(w);
+    w += align_up(m * 4);
+    ra.r_seed = reinterpret_cast<uint16_t *>(w);
+    w += align_up(m * 2);
+    uint16_t *sums = reinterpret_cast<uint16_t *>(w);
+    w += align_up(m * 2);
+    ra.meta = w;
+    const uint32_t blocks = static_cast<uint32_t>(std::min<uint64_t>((n + kBlock - 1) / kBlock, 8192));
+    hipLaunchKernelGGL(rx_parse_kernel, dim3(blocks), dim3(kBlock), 0, st, ra);
+    if (int e = hip_status(hipGetLastError()))
+        return e;
+    CsumArgs a{};
+    set_arena(a, d_arena, arena_bytes);
+    a.off = ra.r_off;
+    a.len = ra.r_len;
+    a.seed = ra.r_seed;
+    a.out = sums;
+    a.n = static_cast<uint32_t>(m);
+    a.flags = RNS_FLAG_COMPLEMENT;
+    if (int e = dispatch<false>(a, 4u, 0u, 0u, 0u, st))  // mixed kernel: headers + segments
+        return e;
+    hipLaunchKernelGGL(rx_verdict_kernel, dim3(blocks), dim3(kBlock), 0, st, ra.meta, sums, n, d_status, d_l4_sum);
     return hip_status(hipGetLastError());
 }
 
