@@ -1,0 +1,145 @@
+"""Device time of the widened §8f operations on MI355X (one GPU), next to the plain
+batch checksum, on the headline batch (2^20 x 1500 B) and on IMIX:
+
+* csum     — rns_csum_batch_dev (the hot path itself)
+* chain    — rns_csum_chain_dev: every packet as the stack receives it after the
+             IP trim, three fragments [492, 512, 496]
+* fill     — rns_csum_fill_dev: transmit fill of the TCP checksum field [16..18]
+* verify   — rns_rx_verify_dev: IPv4 header + TCP checks of whole datagrams
+
+Timing: one pair of HIP events around K back-to-back launches on the launch stream,
+median of R rounds.  GB/s counts algorithmic bytes (payload read + result bytes
+written); descriptor and workspace traffic is not credited.
+
+    python tools/bench_ops.py [--steps 20] [--rounds 5] [--out profiles/r01_ops.json]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from rustnetworkstack_amd.batch import (PreparedBatch, csum_chain, csum_fill, rx_verify)  # noqa: E402
+from rustnetworkstack_amd.workloads import DeviceBatch, make_layout  # noqa: E402
+
+L4 = bytes([192, 168, 1, 2])
+L6 = bytes.fromhex("fe800000000000000000000000000002")
+
+
+def write_ipv4_tcp_headers(b, lay, dev):
+    """IPv4 header (src R4, dst L4, proto 6) in each packet's first 20 bytes, header
+    checksum filled (ip.rs:158-159), TCP checksum filled with the per-packet
+    pseudo-header seed (tcp.rs:957-973)."""
+    from oracle.oracle import pseudo_header_py  # test infrastructure: builds inputs only
+    n = lay.n
+    hdr = np.frombuffer(bytes.fromhex("4500000000004000400600000000000000000000"), dtype=np.uint8).copy()
+    hdr[12:16] = [192, 168, 1, 1]
+    hdr[16:20] = np.frombuffer(L4, dtype=np.uint8)
+    hdrs = np.tile(hdr, (n, 1))
+    hdrs[:, 2] = (lay.length >> 8) & 0xFF
+    hdrs[:, 3] = lay.length & 0xFF
+    idx = b.off.view(-1, 1) + torch.arange(20, device=dev)
+    b.arena[idx.flatten()] = torch.from_numpy(hdrs.reshape(-1)).to(dev)
+    del idx
+    csum_fill(b.arena, b.off, torch.full((n,), 20, dtype=torch.int32, device=dev), None, field_off=10)
+    l4 = lay.length.astype(np.int64) - 20
+    uniq = {int(x): pseudo_header_py(bytes([192, 168, 1, 1]), L4, int(x), 6) for x in np.unique(l4)}
+    seeds = np.array([uniq[int(x)] for x in l4], dtype=np.uint16) if len(uniq) > 1 else \
+        np.full(n, next(iter(uniq.values())), dtype=np.uint16)
+    csum_fill(b.arena, b.off + 20, b.length - 20, torch.from_numpy(seeds.view(np.int16)).to(dev), field_off=16)
+    torch.cuda.synchronize()
+
+
+def timed(fn, steps, rounds):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    fn()
+    res = []
+    for _ in range(rounds):
+        e0.record()
+        for _ in range(steps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        res.append(e0.elapsed_time(e1) / steps)
+    res.sort()
+    return res[len(res) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--configs", default="c3_1500B,c5_imix")
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    results = {}
+    for cfg in args.configs.split(","):
+        lay = make_layout(cfg)
+        b = DeviceBatch(lay, dev)
+        n, pay = lay.n, lay.payload_bytes
+        r = {}
+        pb = PreparedBatch(b.arena, b.off, b.length, b.seed, complement=True, out=b.out,
+                           len_hint=int(round(lay.mean_len)))
+        ms = timed(pb, args.steps, args.rounds)
+        r["csum"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1)}
+        # chain: three fragments per packet where the packet is long enough, else one
+        L = lay.length.astype(np.int64)
+        nfr = np.where(L > 1004, 3, 1)
+        first = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(nfr, out=first[1:])
+        nf = int(first[-1])
+        frag_off = np.empty(nf, dtype=np.uint64)
+        frag_len = np.empty(nf, dtype=np.uint32)
+        three = nfr == 3
+        i3 = first[:-1][three]
+        frag_off[i3] = lay.off[three]
+        frag_off[i3 + 1] = lay.off[three] + 492
+        frag_off[i3 + 2] = lay.off[three] + 1004
+        frag_len[i3] = 492
+        frag_len[i3 + 1] = 512
+        frag_len[i3 + 2] = (L[three] - 1004).astype(np.uint32)
+        i1 = first[:-1][~three]
+        frag_off[i1] = lay.off[~three]
+        frag_len[i1] = lay.length[~three]
+        d_fo = torch.from_numpy(frag_off.view(np.int64)).to(dev)
+        d_fl = torch.from_numpy(frag_len.view(np.int32)).to(dev)
+        d_first = torch.from_numpy(first.astype(np.uint32).view(np.int32)).to(dev)
+        sums = torch.empty(nf, dtype=torch.uint16, device=dev)
+        out = torch.empty(n, dtype=torch.uint16, device=dev)
+        ms = timed(lambda: csum_chain(b.arena, d_fo, d_fl, d_first, b.seed, complement=True, out=out,
+                                      frag_sums=sums, frag_len_hint=int(round(pay / nf))),
+                   args.steps, args.rounds)
+        r["chain"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1),
+                      "fragments": nf}
+        ms = timed(lambda: csum_fill(b.arena, b.off, b.length, b.seed, field_off=16), args.steps, args.rounds)
+        r["fill"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1)}
+        # verify: turn every packet into a valid IPv4/TCP datagram first (header written
+        # on the GPU, IPv4 and TCP checksums filled), so every byte is checked
+        write_ipv4_tcp_headers(b, lay, dev)
+        ws = torch.empty(int(__import__("rustnetworkstack_amd")._lib.load().rns_rx_verify_workspace_bytes(n)),
+                         dtype=torch.uint8, device=dev)
+        st = torch.empty(n, dtype=torch.uint8, device=dev)
+        ms = timed(lambda: rx_verify(b.arena, b.off, b.length, L4, L6, status=st, workspace=ws),
+                   args.steps, args.rounds)
+        accepted = int((st == 0x43).sum().item())
+        r["verify"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + n) / ms / 1e6, 1),
+                       "accepted": accepted, "packets": n}
+        results[cfg] = r
+        print(cfg, json.dumps(r), flush=True)
+        del b
+        torch.cuda.empty_cache()
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump({"tool": "tools/bench_ops.py", "steps": args.steps, "rounds": args.rounds,
+                       "results": results}, f, indent=1)
+    print(json.dumps(results))
+
+
+if __name__ == "__main__":
+    main()
