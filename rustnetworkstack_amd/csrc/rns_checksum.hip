@@ -643,6 +643,8 @@ __global__ __launch_bounds__(kBlock, (BUF && !FILL) ? 4 : 3) void csum_mixed_ker
         if constexpr (FILL) {
             d_field = live ? (a.field ? static_cast<uint32_t>(a.field[p]) : a.field_off) : 0u;
             d_ok = d_ok && d_len >= 2 && d_field <= d_len - 2;  // header[f..f+2] must exist
+            // (stores happen after the wave read all 64 packets: a store between a
+            // prefetch and its consumer would serialise the in-order vmcnt waits)
         }
         const uint64_t own_start = d_start;
         if (!d_ok || d_len == 0) {
