@@ -151,8 +151,8 @@ int rns_csum_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_
  * (tcp.rs:838-850), ICMPv4 (icmp.rs:46-50), ICMPv6 (icmp.rs:62-75); UDP is not
  * verified by the stack (udp.rs:126-148).  As in the reference, the L4 length is
  * the buffer length minus the IP header (the total-length field is not used).
- * d_status[i] gets RNS_RX_* bits; d_l4_sum (optional) the complemented L4 sum.
- * d_workspace: device memory of rns_rx_verify_workspace_bytes(n) bytes. */
+ * One fused pass over the datagram bytes.  d_status[i] gets RNS_RX_* bits;
+ * d_l4_sum (optional) the complemented L4 sum. */
 #define RNS_RX_IP_OK          0x01u  /* IPv4 header checksum verifies (always set for IPv6) */
 #define RNS_RX_L4_OK          0x02u  /* TCP / ICMPv4 / ICMPv6 checksum verifies */
 #define RNS_RX_L4_UNCHECKED   0x04u  /* UDP: the stack does not verify it */
@@ -160,10 +160,9 @@ int rns_csum_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_
 #define RNS_RX_UNKNOWN_PROTO  0x10u  /* protocol the stack drops */
 #define RNS_RX_ACCEPT         0x40u  /* the stack would deliver it to its transport handler */
 #define RNS_RX_MALFORMED      0x80u  /* bad version / too short: the reference drops or panics */
-uint64_t rns_rx_verify_workspace_bytes(uint32_t n);
 int rns_rx_verify_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off, const uint32_t *d_len,
                       uint32_t n, const uint8_t *local_ipv4, const uint8_t *local_ipv6, uint8_t *d_status,
-                      uint16_t *d_l4_sum, void *d_workspace, uint64_t workspace_bytes, void *stream);
+                      uint16_t *d_l4_sum, void *stream);
 
 /* Tuning entry (bench / tests): explicit kernel shape.  variant bit 0: 0 = group
  * kernel (one lane stores each result), 1 = rounds kernel (a wave owns 64

@@ -227,8 +227,7 @@ def csum_fill(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, seed
 
 
 def rx_verify(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, local_ipv4: bytes, local_ipv6: bytes,
-              *, status: torch.Tensor | None = None, l4_sum: torch.Tensor | None = None,
-              workspace: torch.Tensor | None = None) -> torch.Tensor:
+              *, status: torch.Tensor | None = None, l4_sum: torch.Tensor | None = None) -> torch.Tensor:
     """Receive verify of a batch of IP datagrams (rns_rx_verify_dev): returns a uint8
     status per packet (RNS_RX_* bits; RNS_RX_ACCEPT = the stack would deliver it)."""
     _require_cuda(arena, "arena", (torch.uint8,))
@@ -239,9 +238,6 @@ def rx_verify(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, loca
     n = off.numel()
     dev = arena.device
     lib = _lib.load()
-    need = int(lib.rns_rx_verify_workspace_bytes(n))
-    if workspace is None or workspace.numel() < need:
-        workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
     if status is None:
         status = torch.empty(n, dtype=torch.uint8, device=dev)
     l4_ptr = None
@@ -251,7 +247,7 @@ def rx_verify(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, loca
     with torch.cuda.device(dev):
         st = lib.rns_rx_verify_dev(arena.data_ptr(), arena.numel(), off.data_ptr(), length.data_ptr(), n,
                                    bytes(local_ipv4), bytes(local_ipv6), status.data_ptr(), l4_ptr,
-                                   workspace.data_ptr(), workspace.numel(), _stream_handle(dev))
+                                   _stream_handle(dev))
     _lib.check(st, "rns_rx_verify_dev")
     return status
 

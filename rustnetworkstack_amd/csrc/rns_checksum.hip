@@ -55,6 +55,10 @@ struct CsumArgs {
     uint32_t flags;
     const uint16_t *field;     // transmit fill: per-packet checksum field offset (null => field_off)
     uint32_t field_off;
+    uint8_t *status;           // receive verify: RNS_RX_* per datagram
+    uint16_t *l4_out;          // receive verify: complemented L4 sum (optional)
+    uint32_t local4_sum;       // receive verify: BE word sums of the local addresses
+    uint32_t local6_sum;
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -609,21 +613,124 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
         v[u] = w[u];
 }
 
+// ---------------------------------------------------------------------------
+// Receive verify (§8f row 1), fused into the mixed kernel (RX = true): the checks
+// ip_input_v4 (ip.rs:65-92), ip_input_v6 (ip.rs:108-115), ip_input_common
+// (ip.rs:117-128), tcp::validate_checksum (tcp.rs:838-850), icmp_input_v4
+// (icmp.rs:44-50) and icmp_input_v6 (icmp.rs:62-75) apply to a received datagram.
+// A wave takes 32 datagrams; lanes j and j+32 both parse datagram j's header (a few
+// byte loads of lines the data pass reads next), lane j sums the IPv4 header, lane
+// j+32 the L4 segment seeded with the pseudo-header sum (dest = the LOCAL address,
+// as the reference passes netif::get_ipaddr()), and lane j combines both.
+// ---------------------------------------------------------------------------
+enum : uint32_t {
+    kMetaV4 = 1, kMetaV6 = 2, kMetaFrag = 4, kMetaMalformed = 8,
+    kMetaL4Checked = 16, kMetaUnchecked = 32, kMetaUnknown = 64,
+};
+
+__device__ __forceinline__ uint32_t fold16(uint32_t x)
+{
+    while (x > 0xffff)
+        x = (x & 0xffff) + (x >> 16);
+    return x;
+}
+
+struct RxParse {
+    uint32_t meta;  // kMeta* bits
+    uint32_t hdr;   // IP header bytes (IHL*4 or 40)
+    uint32_t ph;    // L4 seed: pseudo-header sum (TCP, ICMPv6) or 0 (ICMPv4)
+};
+
+// p = the datagram's first byte, L = its length (the buffer length, as the stack sees it).
+__device__ __forceinline__ RxParse rx_parse(const uint8_t *p, uint32_t L, uint32_t local4_sum, uint32_t local6_sum)
+{
+    RxParse r{kMetaMalformed, 0u, 0u};
+    if (L == 0)
+        return r;
+    const uint32_t version = p[0] >> 4;                      // ip.rs:40
+    uint32_t proto = 0, src_sum = 0;
+    bool v4src = false;
+    if (version == 4) {
+        r.hdr = (p[0] & 0xf) * 4u;                           // ip.rs:71
+        if (r.hdr == 0 || L < 16 || r.hdr > L)               // empty slice / header index / trim_head panic
+            return r;
+        r.meta = kMetaV4;
+        if (((static_cast<uint32_t>(p[6]) << 8 | p[7]) & 0x3fff) != 0)  // ip.rs:84-87
+            r.meta |= kMetaFrag;
+        proto = p[9];                                        // ip.rs:89
+        src_sum = (static_cast<uint32_t>(p[12]) << 8 | p[13]) + (static_cast<uint32_t>(p[14]) << 8 | p[15]);
+        v4src = true;
+    } else if (version == 6) {
+        r.hdr = 40;
+        if (L < 40)                                          // trim_head(IPV6_HEADER_LEN) would panic
+            return r;
+        r.meta = kMetaV6;
+        proto = p[6];                                        // ip.rs:110
+        for (int k = 8; k < 24; k += 2)                      // source address, ip.rs:111
+            src_sum += static_cast<uint32_t>(p[k]) << 8 | p[k + 1];
+    } else {
+        return r;                                            // "IP: Invalid version field"
+    }
+    const uint32_t l4len = L - r.hdr;                        // packet.len() after trim_head
+    if (proto == 6) {                                        // tcp.rs:838-850: dest = local address of src's family
+        r.ph = v4src ? fold16(src_sum + local4_sum + 6 + (l4len & 0xffff))
+                     : fold16(src_sum + local6_sum + (l4len >> 16) + (l4len & 0xffff) + 6);
+        r.meta |= kMetaL4Checked;
+    } else if (proto == 1) {                                 // icmp.rs:46: no pseudo header
+        r.meta |= kMetaL4Checked;
+    } else if (proto == 58) {                                // icmp.rs:63-68: dest = local IPv6
+        if (v4src) {
+            r.meta = kMetaMalformed;                         // V4 source in a V6 pseudo-header: copy_to panics
+            return r;
+        }
+        r.ph = fold16(src_sum + local6_sum + (l4len >> 16) + (l4len & 0xffff) + 58);
+        r.meta |= kMetaL4Checked;
+    } else if (proto == 17) {
+        r.meta |= kMetaUnchecked;                            // udp.rs:126-148 never verifies
+    } else {
+        r.meta |= kMetaUnknown;                              // ip.rs:126 "Unknown protocol"
+    }
+    return r;
+}
+
+// hdr_res / l4_res: complemented sums (0 = verifies).
+__device__ __forceinline__ uint8_t rx_verdict(uint32_t m, uint32_t hdr_res, uint32_t l4_res)
+{
+    if (m & kMetaMalformed)
+        return RNS_RX_MALFORMED;
+    uint32_t st = 0;
+    if ((m & kMetaV6) || hdr_res == 0)                       // compute_checksum(header) == 0 (ip.rs:76-80)
+        st |= RNS_RX_IP_OK;
+    if (m & kMetaFrag)
+        st |= RNS_RX_FRAGMENT;
+    if ((m & kMetaL4Checked) && l4_res == 0)                 // buffer sum ^ 0xffff == 0
+        st |= RNS_RX_L4_OK;
+    if (m & kMetaUnchecked)
+        st |= RNS_RX_L4_UNCHECKED;
+    if (m & kMetaUnknown)
+        st |= RNS_RX_UNKNOWN_PROTO;
+    if ((st & RNS_RX_IP_OK) && !(st & RNS_RX_FRAGMENT) && (st & (RNS_RX_L4_OK | RNS_RX_L4_UNCHECKED)))
+        st |= RNS_RX_ACCEPT;
+    return static_cast<uint8_t>(st);
+}
+
 // FILL (transmit in-place fill, tcp.rs:957-973 / udp.rs:158-171 / icmp.rs:87-112 /
 // ip.rs:158-159): the 2-byte checksum field of each packet counts as zero while
 // summing, and the owner lane stores the (complemented) result into it, big-endian
 // (set_be16, util.rs:132-135), after the whole wave has read its 64 packets.
-template <bool STRIDED, bool NT, bool BUF, bool FILL>
-__global__ __launch_bounds__(kBlock, (BUF && !FILL) ? 4 : 3) void csum_mixed_kernel(const CsumArgs a)  // <= 128 VGPRs
+template <bool STRIDED, bool NT, bool BUF, bool FILL, bool RX = false>
+__global__ __launch_bounds__(kBlock, (BUF && !FILL && !RX) ? 4 : 3) void csum_mixed_kernel(const CsumArgs a)
 {
+    static_assert(!(FILL && RX) && !(STRIDED && RX), "one mode at a time");
+    constexpr uint32_t kPer = RX ? 32 : 64;  // packets per wave batch (RX: two ranges per datagram)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
 
-    for (uint64_t base = static_cast<uint64_t>(wave) * 64; base < a.n; base += static_cast<uint64_t>(nwaves) * 64) {
-        const uint64_t p = base + lane;
+    for (uint64_t base = static_cast<uint64_t>(wave) * kPer; base < a.n; base += static_cast<uint64_t>(nwaves) * kPer) {
+        const uint64_t p = base + (RX ? (lane & 31) : lane);
         const bool live = p < a.n;
         uint64_t d_start = 0;
         uint32_t d_len = 0, d_seed = 0;
@@ -640,6 +747,24 @@ __global__ __launch_bounds__(kBlock, (BUF && !FILL) ? 4 : 3) void csum_mixed_ker
         d_start += a.base_adjust;
         uint32_t d_field = 0xFFFFFFFFu;
         bool d_ok = d_start <= a.arena_bytes && d_len <= a.arena_bytes - d_start;
+        uint32_t rx_meta = 0;
+        if constexpr (RX) {  // this lane's range: lane < 32 the IPv4 header, lane >= 32 the L4 segment
+            const RxParse rp = (live && d_ok) ? rx_parse(a.arena + d_start, d_len, a.local4_sum, a.local6_sum)
+                                              : RxParse{kMetaMalformed, 0u, 0u};
+            rx_meta = rp.meta;
+            const bool good = !(rp.meta & kMetaMalformed);
+            if (lane < 32) {
+                const bool v4 = good && (rp.meta & kMetaV4);
+                d_len = v4 ? rp.hdr : 0u;
+                d_seed = v4 ? 0u : 0xffffu;  // nothing to check: complemented result 0
+            } else {
+                const bool l4 = good && (rp.meta & kMetaL4Checked);
+                d_start += rp.hdr;
+                d_len = l4 ? d_len - rp.hdr : 0u;
+                d_seed = l4 ? rp.ph : 0xffffu;
+            }
+            d_ok = true;
+        }
         if constexpr (FILL) {
             d_field = live ? (a.field ? static_cast<uint32_t>(a.field[p]) : a.field_off) : 0u;
             d_ok = d_ok && d_len >= 2 && d_field <= d_len - 2;  // header[f..f+2] must exist
@@ -698,6 +823,15 @@ __global__ __launch_bounds__(kBlock, (BUF && !FILL) ? 4 : 3) void csum_mixed_ker
         run_class<4, NT, BUF, FILL>(a, rsrc, cr, next[5], s_start, s_len, s_field, cls == 4, rank, lane, cur, v, mine);
 
         const uint16_t res = finalize(mine, d_start, d_len, d_seed, d_ok, a.flags);
+        if constexpr (RX) {
+            const uint32_t l4_res = static_cast<uint32_t>(__shfl(static_cast<int>(res), static_cast<int>((lane & 31) + 32), 64));
+            if (lane < 32 && live) {
+                a.status[p] = rx_verdict(rx_meta, res, l4_res);
+                if (a.l4_out)
+                    a.l4_out[p] = static_cast<uint16_t>(l4_res);
+            }
+            continue;
+        }
         if (live && a.out)
             a.out[p] = res;  // 64 consecutive u16: one 128-byte store
         if constexpr (FILL) {
@@ -758,160 +892,6 @@ __global__ __launch_bounds__(kBlock) void chain_combine_kernel(const uint64_t *_
                 atomicAdd(bad, 1u);
         }
         out[i] = static_cast<uint16_t>(acc);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Receive verify (§8f row 1): the checks ip_input_v4 (ip.rs:65-92), ip_input_v6
-// (ip.rs:108-115), ip_input_common (ip.rs:117-128), tcp::validate_checksum
-// (tcp.rs:838-850), icmp_input_v4 (icmp.rs:44-50) and icmp_input_v6 (icmp.rs:62-75)
-// apply to a received datagram, for a whole batch:
-//   1. rx_parse_kernel (thread per packet) reads the few header bytes it needs,
-//      forms the pseudo-header sum (util.rs:180-207, dest = the LOCAL address as
-//      the reference passes netif::get_ipaddr()) and emits two byte ranges per
-//      packet: the IPv4 header, and the L4 segment seeded with that sum;
-//   2. the mixed checksum kernel sums the 2n ranges (complemented) in one pass
-//      over the packet bytes (UDP / unknown protocols: the L4 range is empty,
-//      the stack never verifies them, udp.rs:126-148);
-//   3. rx_verdict_kernel turns sums + parse flags into a status byte.
-// ---------------------------------------------------------------------------
-enum : uint8_t {
-    kMetaV4 = 1, kMetaV6 = 2, kMetaFrag = 4, kMetaMalformed = 8,
-    kMetaL4Checked = 16, kMetaUnchecked = 32, kMetaUnknown = 64,
-};
-
-struct RxArgs {
-    const uint8_t *arena;  // caller's base (any alignment; byte loads)
-    uint64_t arena_bytes;
-    const uint64_t *off;
-    const uint32_t *len;
-    uint32_t n;
-    uint32_t local4_sum;   // BE word sum of the local IPv4 address
-    uint32_t local6_sum;   // BE word sum of the local IPv6 address
-    uint64_t *r_off;       // 2n ranges
-    uint32_t *r_len;
-    uint16_t *r_seed;
-    uint8_t *meta;
-};
-
-__device__ __forceinline__ uint32_t fold16(uint32_t x)
-{
-    while (x > 0xffff)
-        x = (x & 0xffff) + (x >> 16);
-    return x;
-}
-
-__global__ __launch_bounds__(kBlock) void rx_parse_kernel(const RxArgs a)
-{
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-        const uint64_t o = a.off[i];
-        const uint32_t L = a.len[i];
-        uint8_t meta = 0;
-        uint32_t hdr = 0, ph = 0;
-        bool l4_read = false;
-        const bool inb = o <= a.arena_bytes && L <= a.arena_bytes - o;
-        if (!inb || L == 0) {
-            meta = kMetaMalformed;
-        } else {
-            const uint8_t *p = a.arena + o;
-            const uint32_t version = p[0] >> 4;                    // ip.rs:40
-            uint32_t proto = 0, src_sum = 0;
-            bool v4src = false;
-            if (version == 4) {
-                hdr = (p[0] & 0xf) * 4u;                           // ip.rs:71
-                if (hdr == 0 || L < 16 || hdr > L) {               // empty slice / header index / trim_head panic
-                    meta = kMetaMalformed;
-                } else {
-                    meta = kMetaV4;
-                    if (((static_cast<uint32_t>(p[6]) << 8 | p[7]) & 0x3fff) != 0)  // ip.rs:84-87
-                        meta |= kMetaFrag;
-                    proto = p[9];                                  // ip.rs:89
-                    src_sum = (static_cast<uint32_t>(p[12]) << 8 | p[13]) + (static_cast<uint32_t>(p[14]) << 8 | p[15]);
-                    v4src = true;
-                }
-            } else if (version == 6) {
-                hdr = 40;
-                if (L < 40) {                                      // trim_head(IPV6_HEADER_LEN) would panic
-                    meta = kMetaMalformed;
-                } else {
-                    meta = kMetaV6;
-                    proto = p[6];                                  // ip.rs:110
-                    for (int k = 8; k < 24; k += 2)                // source address ip.rs:111
-                        src_sum += static_cast<uint32_t>(p[k]) << 8 | p[k + 1];
-                }
-            } else {
-                meta = kMetaMalformed;                             // "IP: Invalid version field"
-            }
-            if (!(meta & kMetaMalformed)) {
-                const uint32_t l4len = L - hdr;                    // packet.len() after trim_head
-                if (proto == 6) {                                  // tcp.rs:838-850: dest = local address of src's family
-                    ph = v4src ? fold16(src_sum + a.local4_sum + 6 + (l4len & 0xffff))
-                               : fold16(src_sum + a.local6_sum + (l4len >> 16) + (l4len & 0xffff) + 6);
-                    meta |= kMetaL4Checked;
-                    l4_read = true;
-                } else if (proto == 1) {                           // icmp.rs:46: no pseudo header
-                    ph = 0;
-                    meta |= kMetaL4Checked;
-                    l4_read = true;
-                } else if (proto == 58) {                          // icmp.rs:63-68: dest = local IPv6
-                    if (v4src) {
-                        meta |= kMetaMalformed;                    // V4 source into a V6 pseudo-header: copy_to panics
-                    } else {
-                        ph = fold16(src_sum + a.local6_sum + (l4len >> 16) + (l4len & 0xffff) + 58);
-                        meta |= kMetaL4Checked;
-                        l4_read = true;
-                    }
-                } else if (proto == 17) {
-                    meta |= kMetaUnchecked;                        // udp.rs:126-148 never verifies
-                } else {
-                    meta |= kMetaUnknown;                          // ip.rs:126 "Unknown protocol"
-                }
-            }
-        }
-        // range 2i: the IPv4 header (checksum over header[..IHL*4], ip.rs:76); an empty
-        // range seeded 0xffff for IPv6 / malformed (complemented result 0: nothing to check)
-        const bool v4 = (meta & kMetaV4) && !(meta & kMetaMalformed);
-        a.r_off[2 * i] = inb ? o : 0;
-        a.r_len[2 * i] = v4 ? hdr : 0u;
-        a.r_seed[2 * i] = v4 ? 0 : 0xffff;
-        // range 2i+1: the L4 segment seeded with the pseudo-header sum
-        const bool l4 = l4_read && !(meta & kMetaMalformed);
-        a.r_off[2 * i + 1] = l4 ? o + hdr : 0;
-        a.r_len[2 * i + 1] = l4 ? L - hdr : 0u;
-        a.r_seed[2 * i + 1] = l4 ? static_cast<uint16_t>(ph) : static_cast<uint16_t>(0xffff);
-        a.meta[i] = meta;
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void rx_verdict_kernel(const uint8_t *__restrict__ meta,
-                                                            const uint16_t *__restrict__ sums, uint32_t n,
-                                                            uint8_t *__restrict__ status,
-                                                            uint16_t *__restrict__ l4_out)
-{
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint8_t m = meta[i];
-        uint8_t st = 0;
-        if (m & kMetaMalformed) {
-            st = RNS_RX_MALFORMED;
-        } else {
-            if ((m & kMetaV6) || sums[2 * i] == 0)       // compute_checksum(header) == 0 (ip.rs:76-80)
-                st |= RNS_RX_IP_OK;
-            if (m & kMetaFrag)
-                st |= RNS_RX_FRAGMENT;
-            if ((m & kMetaL4Checked) && sums[2 * i + 1] == 0)  // buffer sum ^ 0xffff == 0
-                st |= RNS_RX_L4_OK;
-            if (m & kMetaUnchecked)
-                st |= RNS_RX_L4_UNCHECKED;
-            if (m & kMetaUnknown)
-                st |= RNS_RX_UNKNOWN_PROTO;
-            if ((st & RNS_RX_IP_OK) && !(st & RNS_RX_FRAGMENT) && (st & (RNS_RX_L4_OK | RNS_RX_L4_UNCHECKED)))
-                st |= RNS_RX_ACCEPT;
-        }
-        status[i] = st;
-        if (l4_out)
-            l4_out[i] = sums[2 * i + 1];
     }
 }
 
@@ -1225,14 +1205,6 @@ int rns_csum_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_
     return hip_status(hipGetLastError());
 }
 
-static uint64_t align_up(uint64_t x) { return (x + 255) & ~255ull; }
-
-uint64_t rns_rx_verify_workspace_bytes(uint32_t n)
-{
-    const uint64_t m = 2ull * n;
-    return align_up(m * 8) + align_up(m * 4) + align_up(m * 2) + align_up(m * 2) + align_up(n);
-}
-
 static uint32_t be_sum(const uint8_t *p, int nbytes)
 {
     uint32_t s = 0;
@@ -1243,51 +1215,31 @@ static uint32_t be_sum(const uint8_t *p, int nbytes)
 
 int rns_rx_verify_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off, const uint32_t *d_len,
                       uint32_t n, const uint8_t *local_ipv4, const uint8_t *local_ipv6, uint8_t *d_status,
-                      uint16_t *d_l4_sum, void *d_workspace, uint64_t workspace_bytes, void *stream)
+                      uint16_t *d_l4_sum, void *stream)
 {
     if (n == 0)
         return RNS_OK;
-    if (!d_arena || !d_off || !d_len || !d_status || !local_ipv4 || !local_ipv6 || !d_workspace)
-        return RNS_E_INVALID;
-    if (workspace_bytes < rns_rx_verify_workspace_bytes(n))
+    if (!d_arena || !d_off || !d_len || !d_status || !local_ipv4 || !local_ipv6)
         return RNS_E_INVALID;
     if (int st = check_device())
         return st;
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    const uint64_t m = 2ull * n;
-    uint8_t *w = static_cast<uint8_t *>(d_workspace);
-    RxArgs ra{};
-    ra.arena = d_arena;
-    ra.arena_bytes = arena_bytes;
-    ra.off = d_off;
-    ra.len = d_len;
-    ra.n = n;
-    ra.local4_sum = be_sum(local_ipv4, 4);
-    ra.local6_sum = be_sum(local_ipv6, 16);
-    ra.r_off = reinterpret_cast<uint64_t *>(w);
-    w += align_up(m * 8);
-    ra.r_len = reinterpret_cast<uint32_t *>(w);
-    w += align_up(m * 4);
-    ra.r_seed = reinterpret_cast<uint16_t *>(w);
-    w += align_up(m * 2);
-    uint16_t *sums = reinterpret_cast<uint16_t *>(w);
-    w += align_up(m * 2);
-    ra.meta = w;
-    const uint32_t blocks = static_cast<uint32_t>(std::min<uint64_t>((n + kBlock - 1) / kBlock, 8192));
-    hipLaunchKernelGGL(rx_parse_kernel, dim3(blocks), dim3(kBlock), 0, st, ra);
-    if (int e = hip_status(hipGetLastError()))
-        return e;
     CsumArgs a{};
     set_arena(a, d_arena, arena_bytes);
-    a.off = ra.r_off;
-    a.len = ra.r_len;
-    a.seed = ra.r_seed;
-    a.out = sums;
-    a.n = static_cast<uint32_t>(m);
+    a.off = d_off;
+    a.len = d_len;
+    a.n = n;
     a.flags = RNS_FLAG_COMPLEMENT;
-    if (int e = dispatch<false>(a, 4u, 0u, 0u, 0u, st))  // mixed kernel: headers + segments
-        return e;
-    hipLaunchKernelGGL(rx_verdict_kernel, dim3(blocks), dim3(kBlock), 0, st, ra.meta, sums, n, d_status, d_l4_sum);
+    a.status = d_status;
+    a.l4_out = d_l4_sum;
+    a.local4_sum = be_sum(local_ipv4, 4);
+    a.local6_sum = be_sum(local_ipv6, 16);
+    const uint64_t waves = (static_cast<uint64_t>(n) + 31) / 32;  // 32 datagrams per wave
+    const dim3 grid(static_cast<uint32_t>((waves + kBlock / 64 - 1) / (kBlock / 64))), block(kBlock);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (buf_records(a) < kOobOffset)
+        hipLaunchKernelGGL((csum_mixed_kernel<false, true, true, false, true>), grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL((csum_mixed_kernel<false, true, false, false, true>), grid, block, 0, st, a);
     return hip_status(hipGetLastError());
 }
 

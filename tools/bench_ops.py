@@ -122,10 +122,8 @@ def main():
         # verify: turn every packet into a valid IPv4/TCP datagram first (header written
         # on the GPU, IPv4 and TCP checksums filled), so every byte is checked
         write_ipv4_tcp_headers(b, lay, dev)
-        ws = torch.empty(int(__import__("rustnetworkstack_amd")._lib.load().rns_rx_verify_workspace_bytes(n)),
-                         dtype=torch.uint8, device=dev)
         st = torch.empty(n, dtype=torch.uint8, device=dev)
-        ms = timed(lambda: rx_verify(b.arena, b.off, b.length, L4, L6, status=st, workspace=ws),
+        ms = timed(lambda: rx_verify(b.arena, b.off, b.length, L4, L6, status=st),
                    args.steps, args.rounds)
         accepted = int((st == 0x43).sum().item())
         r["verify"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + n) / ms / 1e6, 1),
