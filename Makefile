@@ -19,7 +19,11 @@ $(BUILD)/host_checksum.o: $(CSRC)/host_checksum.cpp include/rns_checksum.h
 	@mkdir -p $(BUILD)
 	g++ $(CXXFLAGS) -Iinclude -c $< -o $@
 
-$(LIB): $(BUILD)/rns_checksum.o $(BUILD)/host_checksum.o
+$(BUILD)/host_io.o: $(CSRC)/host_io.cpp include/rns_checksum.h
+	@mkdir -p $(BUILD)
+	g++ $(CXXFLAGS) -Iinclude -c $< -o $@
+
+$(LIB): $(BUILD)/rns_checksum.o $(BUILD)/host_checksum.o $(BUILD)/host_io.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
 
 oracle:

@@ -49,6 +49,7 @@ extern "C" {
 #define RNS_E_NODEVICE   (-4)  /* no usable gfx950 device / HIP runtime                     */
 #define RNS_E_ORDER      (-5)  /* host batch: offsets not ascending                         */
 #define RNS_E_TOOLARGE   (-6)  /* host batch: one packet larger than the staging chunk      */
+#define RNS_E_IO         (-7)  /* batched I/O: read/write/poll failed (see errno)            */
 #define RNS_E_HIP_BASE   (-1000) /* RNS_E_HIP_BASE - hipError_t: HIP runtime error          */
 
 /* ---- flags for batch calls ---------------------------------------------- */
@@ -187,6 +188,18 @@ int rns_host_ctx_destroy(rns_host_ctx *ctx);
 int rns_csum_batch_host(rns_host_ctx *ctx, const uint8_t *h_arena, uint64_t arena_bytes,
                         const uint64_t *h_off, const uint32_t *h_len, const uint16_t *h_seed,
                         uint16_t *h_out, uint32_t n, uint32_t flags);
+
+/* Batched datagram I/O.  The reference reads / writes one
+ * packet per call on the TUN fd (recv_packet netif.rs:65-83 -> tun_recv tun.c:84-86;
+ * send_packet netif.rs:85-98 -> tun_send tun.c:88-90).  rns_io_recv_batch waits up
+ * to timeout_ms for the first datagram, then reads every datagram already queued
+ * (up to max_pkts) into consecutive slot_bytes slots of h_arena (2048 = the
+ * reference's MRU, netif.rs:66); h_off/h_len describe them.  Returns the number of
+ * datagrams (0 on timeout) or RNS_E_IO.  Works on a TUN fd or any datagram fd.
+ * rns_io_send_batch writes n datagrams; returns how many were written. */
+int rns_io_recv_batch(int fd, uint8_t *h_arena, uint64_t slot_bytes, uint32_t max_pkts, uint64_t *h_off,
+                      uint32_t *h_len, int timeout_ms);
+int rns_io_send_batch(int fd, const uint8_t *h_arena, const uint64_t *h_off, const uint32_t *h_len, uint32_t n);
 
 /* Pinned host memory for arenas handed to rns_csum_batch_host. */
 int rns_host_alloc(uint64_t bytes, void **out);

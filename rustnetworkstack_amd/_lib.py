@@ -20,6 +20,7 @@ RNS_E_BOUNDS = -3
 RNS_E_NODEVICE = -4
 RNS_E_ORDER = -5
 RNS_E_TOOLARGE = -6
+RNS_E_IO = -7
 RNS_E_HIP_BASE = -1000
 RNS_FLAG_COMPLEMENT = 0x1
 RNS_RX_IP_OK = 0x01
@@ -46,6 +47,8 @@ EXPORTED_SYMBOLS = (
     "rns_host_ctx_create",
     "rns_host_ctx_destroy",
     "rns_csum_batch_host",
+    "rns_io_recv_batch",
+    "rns_io_send_batch",
     "rns_host_alloc",
     "rns_host_free",
     "rns_fill_splitmix64_dev",
@@ -98,6 +101,8 @@ _SIGNATURES = {
     "rns_host_ctx_create": (_int, [_int, _u64, _u32, ctypes.POINTER(_vp)]),
     "rns_host_ctx_destroy": (_int, [_vp]),
     "rns_csum_batch_host": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32]),
+    "rns_io_recv_batch": (_int, [_int, _vp, _u64, _u32, _vp, _vp, _int]),
+    "rns_io_send_batch": (_int, [_int, _vp, _vp, _vp, _u32]),
     "rns_host_alloc": (_int, [_u64, ctypes.POINTER(_vp)]),
     "rns_host_free": (_int, [_vp]),
     "rns_fill_splitmix64_dev": (_int, [_vp, _u64, _u64, _vp]),

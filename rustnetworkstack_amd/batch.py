@@ -103,7 +103,13 @@ class PreparedBatch:
 
     def __call__(self) -> torch.Tensor:
         if self.n:
-            st = self._fn(*self._args)
+            # The bound stream handle belongs to self.device (the null stream is 0): launch
+            # with that device current even if the caller has switched devices since.
+            if torch.cuda.current_device() != self.device.index:
+                with torch.cuda.device(self.device):
+                    st = self._fn(*self._args)
+            else:
+                st = self._fn(*self._args)
             if st != _lib.RNS_OK:
                 raise _lib.ChecksumError(st, "rns_csum_batch_dev")
         return self.out
@@ -262,6 +268,36 @@ def fill_splitmix64(buf: torch.Tensor, seed: int) -> torch.Tensor:
                                          _stream_handle(buf.device))
     _lib.check(st, "rns_fill_splitmix64_dev")
     return buf
+
+
+def recv_batch(fd: int, arena: np.ndarray, slot_bytes: int = 2048, max_pkts: int | None = None,
+               timeout_ms: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """Read every queued datagram (after waiting up to ``timeout_ms`` for the first)
+    into consecutive ``slot_bytes`` slots of ``arena`` (rns_io_recv_batch; the batched
+    form of recv_packet, netif.rs:65-83).  Returns (offsets uint64, lengths uint32)."""
+    if arena.dtype != np.uint8 or not arena.flags["C_CONTIGUOUS"]:
+        raise ValueError("arena must be a contiguous uint8 array")
+    cap = arena.shape[0] // slot_bytes
+    max_pkts = cap if max_pkts is None else min(max_pkts, cap)
+    off = np.empty(max(max_pkts, 1), dtype=np.uint64)
+    ln = np.empty(max(max_pkts, 1), dtype=np.uint32)
+    r = _lib.load().rns_io_recv_batch(int(fd), arena.ctypes.data, slot_bytes, max_pkts, off.ctypes.data,
+                                      ln.ctypes.data, int(timeout_ms))
+    if r < 0:
+        raise _lib.ChecksumError(r, "rns_io_recv_batch")
+    return off[:r], ln[:r]
+
+
+def send_batch(fd: int, arena: np.ndarray, off: np.ndarray, length: np.ndarray) -> int:
+    """Write one datagram per packet (rns_io_send_batch; batched send_packet, netif.rs:85-98)."""
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    length = np.ascontiguousarray(length, dtype=np.uint32)
+    r = _lib.load().rns_io_send_batch(int(fd), arena.ctypes.data, off.ctypes.data, length.ctypes.data,
+                                      off.shape[0])
+    if r < 0:
+        raise _lib.ChecksumError(r, "rns_io_send_batch")
+    return r
 
 
 class PinnedBuffer:

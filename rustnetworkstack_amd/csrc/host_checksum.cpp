@@ -142,6 +142,7 @@ const char *rns_strerror(int status)
     case RNS_E_NODEVICE: return "no usable gfx950 device";
     case RNS_E_ORDER: return "packet offsets are not ascending";
     case RNS_E_TOOLARGE: return "packet larger than the staging chunk";
+    case RNS_E_IO: return "datagram I/O failed (errno)";
     default: return status <= RNS_E_HIP_BASE ? "HIP runtime error" : "unknown status";
     }
 }

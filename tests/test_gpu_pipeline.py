@@ -1,0 +1,43 @@
+"""End-to-end batched receive: SOCK_SEQPACKET socketpair (TUN-like datagram fd) ->
+rns_io_recv_batch into pinned MRU slots -> H2D -> fused rns_rx_verify_dev -> verdicts,
+compared with the reference receive path restated in the oracle."""
+import socket
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from rustnetworkstack_amd.batch import send_batch
+from rustnetworkstack_amd.pipeline import RxPipeline
+from test_gpu_rx import make_packets
+from test_rx_oracle import L4, L6
+
+pytestmark = pytest.mark.gpu
+
+
+def test_socket_to_verdicts(oracle):
+    pkts = make_packets(6000, 0xD1CE)
+    lens = np.array([len(p) for p in pkts], dtype=np.uint32)
+    off = np.zeros(len(pkts), dtype=np.uint64)
+    np.cumsum(lens[:-1].astype(np.uint64), out=off[1:])
+    arena = np.frombuffer(b"".join(pkts), dtype=np.uint8).copy()
+    nonempty = lens > 0                      # a zero-length datagram cannot be told from EOF
+    expect = np.array([O.rx_status_ref(p, L4, L6, ones_comp=oracle.compute_ones_comp) for p in pkts],
+                      dtype=np.uint8)[nonempty]
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+    t = threading.Thread(target=send_batch, args=(a.fileno(), arena, off[nonempty], lens[nonempty]))
+    t.start()
+    pipe = RxPipeline(L4, L6, device=0, max_pkts=1024)
+    got_st, got_len = [], []
+    while sum(x.shape[0] for x in got_st) < int(nonempty.sum()):
+        st, ln = pipe.receive(b.fileno(), timeout_ms=2000)
+        assert st.shape[0] > 0, "receive timed out"
+        got_st.append(st)
+        got_len.append(ln.copy())
+    t.join()
+    pipe.close()
+    a.close()
+    b.close()
+    assert np.array_equal(np.concatenate(got_len), lens[nonempty])
+    assert np.array_equal(np.concatenate(got_st), expect)
