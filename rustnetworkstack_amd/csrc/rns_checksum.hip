@@ -836,10 +836,31 @@ __global__ __launch_bounds__(kBlock, (BUF && !FILL && !RX) ? 4 : 3) void csum_mi
             a.out[p] = res;  // 64 consecutive u16: one 128-byte store
         if constexpr (FILL) {
             if (live && d_ok) {  // set_be16(&mut header[f..f+2], checksum)
-                uint8_t *q = const_cast<uint8_t *>(a.arena) + own_start + d_field;
-                if ((reinterpret_cast<uintptr_t>(q) & 1) == 0) {
-                    *reinterpret_cast<uint16_t *>(q) = static_cast<uint16_t>((res >> 8) | (res << 8));
+                uint8_t *arena_w = const_cast<uint8_t *>(a.arena);
+                const uint64_t fpos = own_start + d_field;       // field offset from the aligned arena
+                const uint64_t sec = fpos & ~31ull;              // its 32-byte memory sector
+                const uint32_t be = (res >> 8) | ((res & 0xffu) << 8);
+                if (sec >= own_start && sec + 32 <= own_start + d_len && (fpos & 31) != 31) {
+                    // The whole sector belongs to this packet (packets never overlap), so
+                    // rewrite it entirely: a full-sector write needs no read-modify-write
+                    // at the memory side, unlike a 2-byte masked store.
+                    uint4 *sp = reinterpret_cast<uint4 *>(arena_w + sec);
+                    uint4 lo = sp[0], hi = sp[1];
+                    uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+                    const uint32_t b = static_cast<uint32_t>(fpos & 31);
+#pragma unroll
+                    for (uint32_t k = 0; k < 2; ++k) {  // bytes b and b+1 (same or adjacent dword)
+                        const uint32_t pos = b + k, di = pos >> 2, sh = (pos & 3) * 8;
+                        const uint32_t byte = (be >> (8 * k)) & 0xffu;
+#pragma unroll
+                        for (uint32_t d = 0; d < 8; ++d)
+                            if (d == di)
+                                w[d] = (w[d] & ~(0xffu << sh)) | (byte << sh);
+                    }
+                    sp[0] = make_uint4(w[0], w[1], w[2], w[3]);
+                    sp[1] = make_uint4(w[4], w[5], w[6], w[7]);
                 } else {
+                    uint8_t *q = arena_w + fpos;
                     q[0] = static_cast<uint8_t>(res >> 8);
                     q[1] = static_cast<uint8_t>(res);
                 }
