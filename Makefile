@@ -29,6 +29,14 @@ $(LIB): $(BUILD)/rns_checksum.o $(BUILD)/host_checksum.o $(BUILD)/host_io.o
 oracle:
 	$(MAKE) -C oracle
 
+# A/B experiment build: tiny packets with 2 lanes each in the mixed kernel
+tools/ab/librns_checksum_tinyg2.so: $(CSRC)/rns_checksum.hip $(BUILD)/host_checksum.o $(BUILD)/host_io.o include/rns_checksum.h
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DRNS_TINY_G2 -Iinclude -c $< -o $(BUILD)/rns_checksum_tinyg2.o
+	@mkdir -p tools/ab
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(BUILD)/rns_checksum_tinyg2.o $(BUILD)/host_checksum.o $(BUILD)/host_io.o
+
+ab: tools/ab/librns_checksum_tinyg2.so
+
 # Register / occupancy report for every kernel instantiation.
 resources: $(CSRC)/rns_checksum.hip
 	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -Iinclude -c $< -o /dev/null -Rpass-analysis=kernel-resource-usage
@@ -41,4 +49,4 @@ clean:
 	rm -rf $(BUILD) $(LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle resources asm clean
+.PHONY: all oracle resources asm clean ab

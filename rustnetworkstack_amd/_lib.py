@@ -11,7 +11,8 @@ import os
 import threading
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "librns_checksum.so")
+# RNS_CHECKSUM_LIB overrides the library path (A/B builds in tools/ experiments only).
+LIB_PATH = os.environ.get("RNS_CHECKSUM_LIB") or os.path.join(PKG_DIR, "librns_checksum.so")
 
 RNS_OK = 0
 RNS_E_INVALID = -1

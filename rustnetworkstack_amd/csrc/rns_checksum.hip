@@ -425,7 +425,7 @@ __device__ __forceinline__ uint16_t finalize(uint32_t mine, uint64_t d_start, ui
 template <int G, int U, bool STRIDED, bool NT, bool BUF>
 __global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
 {
-    static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two in [4,64]");
+    static_assert(G >= 2 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two in [2,64]");
     constexpr uint32_t P = 64 / G;  // packets per round
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t sub = lane & (G - 1);
@@ -512,8 +512,13 @@ struct ClassRun {
 // Size classes (16-byte chunks a packet spans) and the shape each class runs with.
 constexpr uint32_t kNumClasses = 5;
 constexpr uint32_t kClassMax[kNumClasses - 1] = {4, 16, 64, 128};  // above the last: jumbo
+#ifdef RNS_TINY_G2
+constexpr uint32_t kClassLog2G[kNumClasses] = {1, 2, 4, 5, 6};     // lanes per packet 2, 4, 16, 32, 64
+constexpr uint32_t kClassU[kNumClasses] = {2, 4, 4, 4, 4};         // chunks in flight per lane
+#else
 constexpr uint32_t kClassLog2G[kNumClasses] = {2, 2, 4, 5, 6};     // lanes per packet 4, 4, 16, 32, 64
 constexpr uint32_t kClassU[kNumClasses] = {1, 4, 4, 4, 4};         // chunks in flight per lane
+#endif
 constexpr int kUMax = 4;
 
 // Round 0 of class n (wave-uniform; kNumClasses = none), issued with the class's
@@ -965,10 +970,14 @@ int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipSt
         else
             hipLaunchKernelGGL((csum_mixed_kernel<S, false, false, false>), grid, block, 0, st, a);
     } else if ((variant & 1) == 0) {
-        if (nt)
-            hipLaunchKernelGGL((csum_batch_kernel<G, U, S, true>), grid, block, 0, st, a);
-        else
-            hipLaunchKernelGGL((csum_batch_kernel<G, U, S, false>), grid, block, 0, st, a);
+        if constexpr (G >= 4) {
+            if (nt)
+                hipLaunchKernelGGL((csum_batch_kernel<G, U, S, true>), grid, block, 0, st, a);
+            else
+                hipLaunchKernelGGL((csum_batch_kernel<G, U, S, false>), grid, block, 0, st, a);
+        } else {
+            return RNS_E_INVALID;
+        }
     } else {
         if (nt && buf)
             hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, true>), grid, block, 0, st, a);
@@ -991,6 +1000,9 @@ int dispatch(const CsumArgs &a, uint32_t variant, uint32_t G, uint32_t U, uint32
         return launch_shape<64, 4, S>(a, variant, max_blocks, st);
 #define RNS_SHAPE(g, u) \
     if (G == g && U == u) return launch_shape<g, u, S>(a, variant, max_blocks, st);
+    if (variant & 1) {  // lanes_per_packet 2: rounds kernel only
+        RNS_SHAPE(2, 1) RNS_SHAPE(2, 2) RNS_SHAPE(2, 4)
+    }
     RNS_SHAPE(4, 1) RNS_SHAPE(4, 2) RNS_SHAPE(4, 4) RNS_SHAPE(4, 8)
     RNS_SHAPE(8, 1) RNS_SHAPE(8, 2) RNS_SHAPE(8, 4) RNS_SHAPE(8, 8)
     RNS_SHAPE(16, 1) RNS_SHAPE(16, 2) RNS_SHAPE(16, 4) RNS_SHAPE(16, 8)
