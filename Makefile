@@ -29,13 +29,18 @@ $(LIB): $(BUILD)/rns_checksum.o $(BUILD)/host_checksum.o $(BUILD)/host_io.o
 oracle:
 	$(MAKE) -C oracle
 
-# A/B experiment build: tiny packets with 2 lanes each in the mixed kernel
-tools/ab/librns_checksum_tinyg2.so: $(CSRC)/rns_checksum.hip $(BUILD)/host_checksum.o $(BUILD)/host_io.o include/rns_checksum.h
-	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DRNS_TINY_G2 -Iinclude -c $< -o $(BUILD)/rns_checksum_tinyg2.o
+# A/B experiment build: `make ab ABDEF=-DRNS_TINY_G2 ABNAME=tinyg2` -> tools/ab/librns_checksum_tinyg2.so
+# (load it with RNS_CHECKSUM_LIB=...).  RNS_TINY_G2: tiny packets with 2 lanes each in
+# the mixed kernel; RNS_RX_PLAIN: receive verify with plain (temporal) loads.
+ABDEF  ?= -DRNS_TINY_G2
+ABNAME ?= tinyg2
+AB_LIB := tools/ab/librns_checksum_$(ABNAME).so
+$(AB_LIB): $(CSRC)/rns_checksum.hip $(BUILD)/host_checksum.o $(BUILD)/host_io.o include/rns_checksum.h
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) $(ABDEF) -Iinclude -c $< -o $(BUILD)/rns_checksum_$(ABNAME).o
 	@mkdir -p tools/ab
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(BUILD)/rns_checksum_tinyg2.o $(BUILD)/host_checksum.o $(BUILD)/host_io.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(BUILD)/rns_checksum_$(ABNAME).o $(BUILD)/host_checksum.o $(BUILD)/host_io.o
 
-ab: tools/ab/librns_checksum_tinyg2.so
+ab: $(AB_LIB)
 
 # Register / occupancy report for every kernel instantiation.
 resources: $(CSRC)/rns_checksum.hip

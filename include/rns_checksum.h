@@ -189,6 +189,36 @@ int rns_csum_batch_host(rns_host_ctx *ctx, const uint8_t *h_arena, uint64_t aren
                         const uint64_t *h_off, const uint32_t *h_len, const uint16_t *h_seed,
                         uint16_t *h_out, uint32_t n, uint32_t flags);
 
+/* Multi-GPU batches.  Packets are independent, so the
+ * batch is cut into contiguous packet ranges of about equal bytes, one per GPU,
+ * with no collective: each GPU's results go straight to their slice of the output.
+ * rns_csum_batch_multi_host: a host-resident batch over one staging context per
+ * device (devices[] may repeat a device), ranges run concurrently, synchronous.
+ * rns_csum_batch_multi_dev: each GPU's shard is already in its own HBM; launches
+ * every shard on its device and stream and returns (asynchronous, like
+ * rns_csum_batch_dev); the calling thread's current device is restored. */
+typedef struct rns_multi_ctx rns_multi_ctx;
+int rns_multi_ctx_create(const int *devices, uint32_t ndev, uint64_t chunk_bytes, uint32_t nstreams,
+                         rns_multi_ctx **out);
+int rns_multi_ctx_destroy(rns_multi_ctx *ctx);
+int rns_csum_batch_multi_host(rns_multi_ctx *ctx, const uint8_t *h_arena, uint64_t arena_bytes,
+                              const uint64_t *h_off, const uint32_t *h_len, const uint16_t *h_seed,
+                              uint16_t *h_out, uint32_t n, uint32_t flags);
+typedef struct rns_dev_batch {
+    int device;                 /* HIP device of this shard */
+    const uint8_t *d_arena;     /* this shard's arena, on `device` */
+    uint64_t arena_bytes;
+    const uint64_t *d_off;
+    const uint32_t *d_len;
+    const uint16_t *d_seed;     /* NULL: seed 0 */
+    uint16_t *d_out;
+    uint32_t n;
+    uint32_t len_hint;          /* as rns_csum_batch_dev */
+    uint32_t *d_bad;            /* optional */
+    void *stream;               /* a stream of `device` (NULL: its default stream) */
+} rns_dev_batch;
+int rns_csum_batch_multi_dev(const rns_dev_batch *batches, uint32_t nbatches, uint32_t flags);
+
 /* Batched datagram I/O.  The reference reads / writes one
  * packet per call on the TUN fd (recv_packet netif.rs:65-83 -> tun_recv tun.c:84-86;
  * send_packet netif.rs:85-98 -> tun_send tun.c:88-90).  rns_io_recv_batch waits up

@@ -84,7 +84,15 @@ RX_IP_OK, RX_L4_OK, RX_L4_UNCHECKED, RX_FRAGMENT, RX_UNKNOWN, RX_ACCEPT, RX_MALF
 
 
 def rx_status_ref(pkt: bytes, local4: bytes, local6: bytes, ones_comp=None) -> int:
-    """What the reference's receive path decides for one datagram, as status bits.
+    """What the reference's receive path decides for one datagram, as status bits
+    (see rx_verify_ref)."""
+    return rx_verify_ref(pkt, local4, local6, ones_comp)[0]
+
+
+def rx_verify_ref(pkt: bytes, local4: bytes, local6: bytes, ones_comp=None) -> tuple:
+    """(status bits, complemented L4 sum) the reference's receive path computes for
+    one datagram; the L4 value is 0 where the stack checks no L4 checksum (UDP,
+    unknown protocols, malformed datagrams).
 
     ip_input (ip.rs:38-48) -> ip_input_v4 (ip.rs:65-92: header checksum over
     header[..IHL*4], fragment drop, protocol header[9], source header[12..16],
@@ -100,12 +108,12 @@ def rx_status_ref(pkt: bytes, local4: bytes, local6: bytes, ones_comp=None) -> i
     oc = ones_comp or ones_comp_py
     L = len(pkt)
     if L == 0:
-        return RX_MALFORMED
+        return RX_MALFORMED, 0
     version = pkt[0] >> 4
     if version == 4:
         hdr = (pkt[0] & 0xF) * 4
         if hdr == 0 or L < 16 or hdr > L:
-            return RX_MALFORMED
+            return RX_MALFORMED, 0
         st = RX_IP_OK if (0xFFFF ^ oc(0, pkt[:hdr])) == 0 else 0
         if ((pkt[6] << 8 | pkt[7]) & 0x3FFF) != 0:
             st |= RX_FRAGMENT
@@ -113,33 +121,36 @@ def rx_status_ref(pkt: bytes, local4: bytes, local6: bytes, ones_comp=None) -> i
     elif version == 6:
         hdr = 40
         if L < 40:
-            return RX_MALFORMED
+            return RX_MALFORMED, 0
         st = RX_IP_OK
         proto, src = pkt[6], pkt[8:24]
     else:
-        return RX_MALFORMED
+        return RX_MALFORMED, 0
     seg = pkt[hdr:]
 
     def buf_sum(seed):  # compute_buffer_ones_comp over a one-fragment buffer; empty buffer -> seed
         return oc(seed, seg) if len(seg) else seed
 
+    l4 = 0
     if proto == 6:
         dst = local4 if len(src) == 4 else local6
-        ok = (buf_sum(pseudo_header_py(src, dst, len(seg), 6)) ^ 0xFFFF) == 0
-        st |= RX_L4_OK if ok else 0
+        l4 = buf_sum(pseudo_header_py(src, dst, len(seg), 6)) ^ 0xFFFF
+        st |= RX_L4_OK if l4 == 0 else 0
     elif proto == 1:
-        st |= RX_L4_OK if (buf_sum(0) ^ 0xFFFF) == 0 else 0
+        l4 = buf_sum(0) ^ 0xFFFF
+        st |= RX_L4_OK if l4 == 0 else 0
     elif proto == 58:
         if len(src) == 4:
-            return RX_MALFORMED
-        st |= RX_L4_OK if (buf_sum(pseudo_header_py(src, local6, len(seg), 58)) ^ 0xFFFF) == 0 else 0
+            return RX_MALFORMED, 0
+        l4 = buf_sum(pseudo_header_py(src, local6, len(seg), 58)) ^ 0xFFFF
+        st |= RX_L4_OK if l4 == 0 else 0
     elif proto == 17:
         st |= RX_L4_UNCHECKED
     else:
         st |= RX_UNKNOWN
     if (st & RX_IP_OK) and not (st & RX_FRAGMENT) and (st & (RX_L4_OK | RX_L4_UNCHECKED)):
         st |= RX_ACCEPT
-    return st
+    return st, l4
 
 
 # --------------------------------------------------------------------------

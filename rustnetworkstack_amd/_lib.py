@@ -48,6 +48,10 @@ EXPORTED_SYMBOLS = (
     "rns_host_ctx_create",
     "rns_host_ctx_destroy",
     "rns_csum_batch_host",
+    "rns_multi_ctx_create",
+    "rns_multi_ctx_destroy",
+    "rns_csum_batch_multi_host",
+    "rns_csum_batch_multi_dev",
     "rns_io_recv_batch",
     "rns_io_send_batch",
     "rns_host_alloc",
@@ -81,6 +85,14 @@ class RnsIpAddr(ctypes.Structure):
     _fields_ = [("version", ctypes.c_uint32), ("bytes", ctypes.c_uint8 * 16)]
 
 
+class RnsDevBatch(ctypes.Structure):
+    """`rns_dev_batch`: one GPU's shard for rns_csum_batch_multi_dev."""
+    _fields_ = [("device", ctypes.c_int), ("d_arena", ctypes.c_void_p), ("arena_bytes", ctypes.c_uint64),
+                ("d_off", ctypes.c_void_p), ("d_len", ctypes.c_void_p), ("d_seed", ctypes.c_void_p),
+                ("d_out", ctypes.c_void_p), ("n", ctypes.c_uint32), ("len_hint", ctypes.c_uint32),
+                ("d_bad", ctypes.c_void_p), ("stream", ctypes.c_void_p)]
+
+
 _LIB = None
 _LOCK = threading.Lock()
 
@@ -102,6 +114,10 @@ _SIGNATURES = {
     "rns_host_ctx_create": (_int, [_int, _u64, _u32, ctypes.POINTER(_vp)]),
     "rns_host_ctx_destroy": (_int, [_vp]),
     "rns_csum_batch_host": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32]),
+    "rns_multi_ctx_create": (_int, [ctypes.POINTER(ctypes.c_int), _u32, _u64, _u32, ctypes.POINTER(_vp)]),
+    "rns_multi_ctx_destroy": (_int, [_vp]),
+    "rns_csum_batch_multi_host": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32]),
+    "rns_csum_batch_multi_dev": (_int, [ctypes.POINTER(RnsDevBatch), _u32, _u32]),
     "rns_io_recv_batch": (_int, [_int, _vp, _u64, _u32, _vp, _vp, _int]),
     "rns_io_send_batch": (_int, [_int, _vp, _vp, _vp, _u32]),
     "rns_host_alloc": (_int, [_u64, ctypes.POINTER(_vp)]),

@@ -362,3 +362,75 @@ class HostBatcher:
             self.close()
         except Exception:
             pass
+
+
+class MultiHostBatcher(HostBatcher):
+    """Host-resident batches over several GPUs (rns_csum_batch_multi_host): the
+    batch is cut into contiguous packet ranges of about equal bytes, one per entry
+    of ``devices`` (a device may repeat), each through its own staging context."""
+
+    def __init__(self, devices, chunk_bytes: int = 64 << 20, nstreams: int = 3):
+        lib = _lib.load()
+        devs = (ctypes.c_int * len(devices))(*devices)
+        ctx = ctypes.c_void_p()
+        _lib.check(lib.rns_multi_ctx_create(devs, len(devices), chunk_bytes, nstreams, ctypes.byref(ctx)),
+                   "rns_multi_ctx_create")
+        self.ctx = ctx.value
+        self.devices = list(devices)
+
+    def run(self, arena: np.ndarray, off: np.ndarray, length: np.ndarray, seed: np.ndarray | None = None,
+            complement: bool = False, out: np.ndarray | None = None) -> np.ndarray:
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        n = off.shape[0]
+        if out is None:
+            out = np.empty(n, dtype=np.uint16)
+        sp = None
+        if seed is not None:
+            seed = np.ascontiguousarray(seed, dtype=np.uint16)
+            sp = seed.ctypes.data
+        st = _lib.load().rns_csum_batch_multi_host(self.ctx, arena.ctypes.data, arena.shape[0], off.ctypes.data,
+                                                   length.ctypes.data, sp, out.ctypes.data, n,
+                                                   _lib.RNS_FLAG_COMPLEMENT if complement else 0)
+        _lib.check(st, "rns_csum_batch_multi_host")
+        return out
+
+    def close(self) -> None:
+        if self.ctx:
+            _lib.load().rns_multi_ctx_destroy(self.ctx)
+            self.ctx = None
+
+
+def csum_batch_multi_dev(shards, *, complement: bool = False) -> None:
+    """Launch every GPU's shard (rns_csum_batch_multi_dev).  ``shards``: a sequence of
+    dicts with keys arena, off, length, out (torch tensors on that shard's device)
+    and optional seed, len_hint, stream.  Asynchronous on each device's stream."""
+    arr = (_lib.RnsDevBatch * len(shards))()
+    keep = []
+    for k, sh in enumerate(shards):
+        arena, off, length, out = sh["arena"], sh["off"], sh["length"], sh["out"]
+        seed = sh.get("seed")
+        for t, name, dt in ((arena, "arena", (torch.uint8,)), (off, "off", (torch.int64,)),
+                            (length, "length", (torch.int32,)), (out, "out", _U16)):
+            _require_cuda(t, name, dt)
+        if seed is not None:
+            _require_cuda(seed, "seed", _U16)
+        n = off.shape[0]
+        if length.shape[0] != n or out.shape[0] < n or (seed is not None and seed.shape[0] < n):
+            raise ValueError(f"shard {k}: descriptor arrays disagree in length")
+        dev = arena.device.index
+        if any(t.device != arena.device for t in (off, length, out)):
+            raise ValueError(f"shard {k}: tensors on different devices")
+        stream = sh.get("stream")
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        hint = sh.get("len_hint")
+        if hint is None:
+            hint = int(length.float().mean().item()) if n else 0
+        arr[k] = _lib.RnsDevBatch(dev, arena.data_ptr(), arena.numel(), off.data_ptr(), length.data_ptr(),
+                                  seed.data_ptr() if seed is not None else None, out.data_ptr(), n, hint, None,
+                                  stream.cuda_stream)
+        keep.append(sh)
+    flags = _lib.RNS_FLAG_COMPLEMENT if complement else 0
+    _lib.check(_lib.load().rns_csum_batch_multi_dev(arr, len(shards), flags), "rns_csum_batch_multi_dev")

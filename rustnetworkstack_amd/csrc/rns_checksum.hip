@@ -31,6 +31,8 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "rns_checksum.h"
@@ -249,16 +251,20 @@ struct Pkt {
     bool big;             // > kNoWrapBytes: exact big-endian path
     int hole;             // transmit fill: the 2-byte checksum field, as a byte index from
                           // chunk 0's first byte (counted as zero while summing); kNoHole: none
+    int split;            // receive verify: bytes before this index (from chunk 0's first byte)
+                          // are the IP header and go to a separate sum; == s: no header bytes
 };
 
 constexpr int kNoHole = -4096;
 
-__device__ __forceinline__ Pkt make_pkt(uint64_t start, uint32_t L, uint32_t field = 0xFFFFFFFFu)
+__device__ __forceinline__ Pkt make_pkt(uint64_t start, uint32_t L, uint32_t field = 0xFFFFFFFFu,
+                                        uint32_t split = 0u)
 {
     Pkt k;
     k.start = start;
     k.hole = (field < L) ? static_cast<int>(start & 15) + static_cast<int>(field) : kNoHole;
     k.s = static_cast<int>(k.start & 15);
+    k.split = k.s + static_cast<int>(min(split, 4096u));
     const uint64_t span = static_cast<uint64_t>(k.s) + L;
     k.nch = L ? static_cast<uint32_t>((span + 15) >> 4) : 0u;
     k.e = static_cast<int>(span - (static_cast<uint64_t>(k.nch ? k.nch - 1 : 0) << 4));
@@ -266,14 +272,15 @@ __device__ __forceinline__ Pkt make_pkt(uint64_t start, uint32_t L, uint32_t fie
     return k;
 }
 
-template <int G, bool HOLE = false>
-__device__ __forceinline__ Pkt fetch_pkt(uint64_t d_start, uint32_t d_len, uint32_t src, uint32_t d_field = 0xFFFFFFFFu)
+// d_aux: the hole's field offset (HOLE) or the header length (SPLIT).
+template <int G, bool HOLE = false, bool SPLIT = false>
+__device__ __forceinline__ Pkt fetch_pkt(uint64_t d_start, uint32_t d_len, uint32_t src, uint32_t d_aux = 0xFFFFFFFFu)
 {
     const uint32_t lo = bcast_from<G>(static_cast<uint32_t>(d_start), src);
     const uint32_t hi = bcast_from<G>(static_cast<uint32_t>(d_start >> 32), src);
     const uint32_t L = bcast_from<G>(d_len, src);
-    const uint32_t f = HOLE ? bcast_from<G>(d_field, src) : 0xFFFFFFFFu;
-    return make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L, f);
+    const uint32_t x = (HOLE || SPLIT) ? bcast_from<G>(d_aux, src) : 0xFFFFFFFFu;
+    return make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L, HOLE ? x : 0xFFFFFFFFu, SPLIT ? x : 0u);
 }
 
 // Loads of one pass: chunk c = c0 + u*G of the packet, for u < U.  Branch-free:
@@ -370,18 +377,44 @@ __device__ __forceinline__ void sum_be(const uint4 (&v)[N], uint32_t w_hi, uint3
     }
 }
 
+// Receive verify: move the IP-header bytes of each chunk (index < k.split) out of
+// v into the header's own LE sum.  Only the first few chunks of a datagram hold
+// header bytes (IHL*4 <= 60), so the branch is rarely taken.
+template <int G, int U, int N = U>
+__device__ __forceinline__ void split_header(const Pkt &k, uint32_t c0, uint4 (&v)[N], uint32_t &hdr)
+{
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int b = k.split - 16 * static_cast<int>(c0 + u * G);  // header bytes in this chunk
+        if (b > 0) {
+            const uint4 h = make_uint4(keep_bytes(v[u].x, 0, b, 0), keep_bytes(v[u].y, 0, b, 4),
+                                       keep_bytes(v[u].z, 0, b, 8), keep_bytes(v[u].w, 0, b, 12));
+            hdr = __builtin_amdgcn_sad_u16(h.x, 0, hdr);
+            hdr = __builtin_amdgcn_sad_u16(h.y, 0, hdr);
+            hdr = __builtin_amdgcn_sad_u16(h.z, 0, hdr);
+            hdr = __builtin_amdgcn_sad_u16(h.w, 0, hdr);
+            v[u] = make_uint4(v[u].x ^ h.x, v[u].y ^ h.y, v[u].z ^ h.z, v[u].w ^ h.w);
+        }
+    }
+}
+
 // One packet's contribution from this lane.  `v` holds the (prefetched) first pass.
-template <int G, int U, bool NT, bool BUF, int N = U, bool HOLE = false>
+// SPLIT: the bytes before k.split are summed into `hdr` (LE) instead.
+template <int G, int U, bool NT, bool BUF, int N = U, bool HOLE = false, bool SPLIT = false>
 __device__ __forceinline__ uint32_t packet_partial(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, const Pkt &k,
-                                                   uint32_t sub, uint4 (&v)[N])
+                                                   uint32_t sub, uint4 (&v)[N], uint32_t &hdr)
 {
     constexpr uint32_t kPass = G * U;
     mask_edges<G, U, N, HOLE>(k, sub, v);
+    if constexpr (SPLIT)
+        split_header<G, U, N>(k, sub, v, hdr);
     if (!k.big) {
         uint32_t acc = sum_le<U, N>(v, 0u);
         for (uint32_t c0 = kPass + sub; c0 < k.nch; c0 += kPass) {  // packets longer than one pass (reuse v)
             issue_pass<G, U, NT, BUF, N>(a, rsrc, k, c0, v);
             mask_edges<G, U, N, HOLE>(k, c0, v);
+            if constexpr (SPLIT)
+                split_header<G, U, N>(k, c0, v, hdr);
             acc = sum_le<U, N>(v, acc);
         }
         return acc;  // LE-word sum, exact (< 2^32 for a packet of <= 128 KiB)
@@ -392,24 +425,27 @@ __device__ __forceinline__ uint32_t packet_partial(const CsumArgs &a, __amdgpu_b
     for (uint32_t c0 = kPass + sub; c0 < k.nch; c0 += kPass) {
         issue_pass<G, U, NT, BUF, N>(a, rsrc, k, c0, v);
         mask_edges<G, U, N, HOLE>(k, c0, v);
+        if constexpr (SPLIT)
+            split_header<G, U, N>(k, c0, v, hdr);
         sum_be<U, N>(v, w_hi, hs, ls);
     }
     return (hs << 8) + ls;  // BE-word sum mod 2^32, exactly the reference's accumulator
 }
 
 // Owner-lane finish: seed + this packet's word sum -> the reference's folded u16.
-__device__ __forceinline__ uint16_t finalize(uint32_t mine, uint64_t d_start, uint32_t d_len, uint32_t d_seed,
-                                             bool d_ok, uint32_t flags)
+// odd: the packet starts at an odd offset; big: longer than kNoWrapBytes (BE sum).
+__device__ __forceinline__ uint16_t finalize_bits(uint32_t mine, bool odd, bool big, uint32_t d_seed, bool d_ok,
+                                                  uint32_t flags)
 {
     uint32_t acc;
-    if (d_len <= kNoWrapBytes) {
+    if (!big) {
         // seed + BE words, no wrap possible: equals seed + G where G is the LE
         // sum folded and byte-swapped (a packet at an odd offset is already in
         // BE order relative to the aligned words) — RFC 1071 §2(B).
         uint32_t x = mine;
         while (x > 0xffff)
             x = (x & 0xffff) + (x >> 16);
-        const uint32_t g = (d_start & 1) ? x : (((x & 0xff) << 8) | (x >> 8));
+        const uint32_t g = odd ? x : (((x & 0xff) << 8) | (x >> 8));
         acc = d_seed + g;
         acc = (acc & 0xffff) + (acc >> 16);  // <= 0x1fffe: one end-around step folds it
     } else {
@@ -420,6 +456,12 @@ __device__ __forceinline__ uint16_t finalize(uint32_t mine, uint64_t d_start, ui
     if (flags & RNS_FLAG_COMPLEMENT)
         acc ^= 0xffff;
     return d_ok ? static_cast<uint16_t>(acc) : static_cast<uint16_t>(0);
+}
+
+__device__ __forceinline__ uint16_t finalize(uint32_t mine, uint64_t d_start, uint32_t d_len, uint32_t d_seed,
+                                             bool d_ok, uint32_t flags)
+{
+    return finalize_bits(mine, d_start & 1, d_len > kNoWrapBytes, d_seed, d_ok, flags);
 }
 
 template <int G, int U, bool STRIDED, bool NT, bool BUF>
@@ -472,7 +514,8 @@ __global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
             nxt.nch = has_next ? nxt.nch : 0u;
             uint4 w[U];
             issue_pass<G, U, NT, BUF>(a, rsrc, nxt, sub, w);
-            const uint32_t words = group_allreduce<G>(packet_partial<G, U, NT, BUF>(a, rsrc, cur, sub, v));
+            uint32_t unused = 0;
+            const uint32_t words = group_allreduce<G>(packet_partial<G, U, NT, BUF>(a, rsrc, cur, sub, v, unused));
             if constexpr (G == 64) {
                 mine = (lane == r) ? words : mine;
             } else {
@@ -524,10 +567,10 @@ constexpr int kUMax = 4;
 // Round 0 of class n (wave-uniform; kNumClasses = none), issued with the class's
 // runtime shape into the shared buffer: the last round of the previous class
 // calls this, so a class starts with its first pass already in flight.
-template <bool NT, bool BUF, bool FILL>
+template <bool NT, bool BUF, bool FILL, bool RX>
 __device__ __forceinline__ Pkt prefetch_class(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint32_t n,
                                               const ClassRun (&cr)[kNumClasses], uint64_t s_start, uint32_t s_len,
-                                              uint32_t s_field, uint32_t lane, uint4 (&w)[kUMax])
+                                              uint32_t s_aux, uint32_t lane, uint4 (&w)[kUMax])
 {
     uint32_t lg = 6, U = 0, off = 0, cnt = 0;
 #pragma unroll
@@ -546,8 +589,8 @@ __device__ __forceinline__ Pkt prefetch_class(const CsumArgs &a, __amdgpu_buffer
     const uint32_t lo = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(s_start)), src, 64));
     const uint32_t hi = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(s_start >> 32)), src, 64));
     const uint32_t L = static_cast<uint32_t>(__shfl(static_cast<int>(s_len), src, 64));
-    const uint32_t f = FILL ? static_cast<uint32_t>(__shfl(static_cast<int>(s_field), src, 64)) : 0xFFFFFFFFu;
-    Pkt k = make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L, f);
+    const uint32_t x = (FILL || RX) ? static_cast<uint32_t>(__shfl(static_cast<int>(s_aux), src, 64)) : 0xFFFFFFFFu;
+    Pkt k = make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L, FILL ? x : 0xFFFFFFFFu, RX ? x : 0u);
     k.nch = valid ? k.nch : 0u;
     const uint64_t first = k.start - static_cast<uint64_t>(k.s);
 #pragma unroll
@@ -568,11 +611,12 @@ __device__ __forceinline__ Pkt prefetch_class(const CsumArgs &a, __amdgpu_buffer
 
 // All rounds of class C.  On entry (cur, v) hold round 0's prefetched first pass;
 // on exit they hold the first pass of class `next` (the next non-empty class).
-template <uint32_t C, bool NT, bool BUF, bool FILL>
+template <uint32_t C, bool NT, bool BUF, bool FILL, bool RX>
 __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc,
                                           const ClassRun (&cr)[kNumClasses], uint32_t next, uint64_t s_start,
-                                          uint32_t s_len, uint32_t s_field, bool in_class, uint32_t rank,
-                                          uint32_t lane, Pkt &cur, uint4 (&v)[kUMax], uint32_t &mine)
+                                          uint32_t s_len, uint32_t s_aux, bool in_class, uint32_t rank,
+                                          uint32_t lane, Pkt &cur, uint4 (&v)[kUMax], uint32_t &mine,
+                                          uint32_t &mine_hdr)
 {
     constexpr int G = 1 << kClassLog2G[C];
     constexpr int U = static_cast<int>(kClassU[C]);
@@ -584,19 +628,28 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
         return;  // (cur, v) already hold the next class's prefetch
     auto fetch = [&](uint32_t r) {  // group `grp` of round r: sorted position off + r*P + grp
         const uint32_t i = r * P + grp;
-        Pkt k = fetch_pkt<G, FILL>(s_start, s_len, cr[C].off + (i < cr[C].cnt ? i : 0), s_field);
+        Pkt k = fetch_pkt<G, FILL, RX>(s_start, s_len, cr[C].off + (i < cr[C].cnt ? i : 0), s_aux);
         k.nch = (i < cr[C].cnt) ? k.nch : 0u;
         return k;
     };
     auto finish = [&](uint32_t r) {  // consume round r from (cur, v), route each sum to its owner lane
+        uint32_t hdr = 0;
         const uint32_t words =
-            group_allreduce<G>(packet_partial<G, U, NT, BUF, kUMax, FILL>(a, rsrc, cur, sub, v));
+            group_allreduce<G>(packet_partial<G, U, NT, BUF, kUMax, FILL, RX>(a, rsrc, cur, sub, v, hdr));
+        if constexpr (RX)
+            hdr = group_allreduce<G>(hdr);
         if constexpr (G == 64) {
             mine = (in_class && rank == r) ? words : mine;  // wave-uniform sum
+            if constexpr (RX)
+                mine_hdr = (in_class && rank == r) ? hdr : mine_hdr;
         } else {
-            const uint32_t t =
-                static_cast<uint32_t>(__shfl(static_cast<int>(words), static_cast<int>((rank % P) * G), 64));
+            const int src = static_cast<int>((rank % P) * G);
+            const uint32_t t = static_cast<uint32_t>(__shfl(static_cast<int>(words), src, 64));
             mine = (in_class && rank / P == r) ? t : mine;
+            if constexpr (RX) {
+                const uint32_t th = static_cast<uint32_t>(__shfl(static_cast<int>(hdr), src, 64));
+                mine_hdr = (in_class && rank / P == r) ? th : mine_hdr;
+            }
         }
     };
     for (uint32_t r = 0; r + 1 < rounds; ++r) {
@@ -610,7 +663,7 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
             v[u] = w[u];
     }
     uint4 w[kUMax];
-    const Pkt nxt = prefetch_class<NT, BUF, FILL>(a, rsrc, next, cr, s_start, s_len, s_field, lane, w);
+    const Pkt nxt = prefetch_class<NT, BUF, FILL, RX>(a, rsrc, next, cr, s_start, s_len, s_aux, lane, w);
     finish(rounds - 1);
     cur = nxt;
 #pragma unroll
@@ -623,10 +676,15 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
 // ip_input_v4 (ip.rs:65-92), ip_input_v6 (ip.rs:108-115), ip_input_common
 // (ip.rs:117-128), tcp::validate_checksum (tcp.rs:838-850), icmp_input_v4
 // (icmp.rs:44-50) and icmp_input_v6 (icmp.rs:62-75) apply to a received datagram.
-// A wave takes 32 datagrams; lanes j and j+32 both parse datagram j's header (a few
-// byte loads of lines the data pass reads next), lane j sums the IPv4 header, lane
-// j+32 the L4 segment seeded with the pseudo-header sum (dest = the LOCAL address,
-// as the reference passes netif::get_ipaddr()), and lane j combines both.
+// A wave takes 64 datagrams, one per owner lane, which parses its header (a few byte
+// loads of lines the data pass reads next) and turns it into ONE byte range and a
+// split point: IPv4 with a checked L4 -> the whole datagram, split at IHL*4; IPv4
+// otherwise -> the header alone; IPv6 with a checked L4 -> the L4 segment (no header
+// checksum in IPv6).  The data pass sums the bytes before the split (the header) and
+// after it (the L4 segment, seeded with the pseudo-header sum: dest = the LOCAL
+// address, as the reference passes netif::get_ipaddr()) separately, and the owner
+// lane combines both.  The split is even (IHL*4 or 40), so both parts pair their
+// bytes exactly as the reference's separate calls do.
 // ---------------------------------------------------------------------------
 enum : uint32_t {
     kMetaV4 = 1, kMetaV6 = 2, kMetaFrag = 4, kMetaMalformed = 8,
@@ -646,33 +704,73 @@ struct RxParse {
     uint32_t ph;    // L4 seed: pseudo-header sum (TCP, ICMPv6) or 0 (ICMPv4)
 };
 
-// p = the datagram's first byte, L = its length (the buffer length, as the stack sees it).
-__device__ __forceinline__ RxParse rx_parse(const uint8_t *p, uint32_t L, uint32_t local4_sum, uint32_t local6_sum)
+// The first 24 bytes of a datagram (every field rx_parse reads) as six dwords in
+// datagram byte order, from the three aligned 16-byte chunks around them, all
+// loaded at once (one memory latency, where per-field byte loads took two
+// dependent ones).  Bytes past the datagram are not used: rx_parse checks L first.
+template <bool BUF>
+__device__ __forceinline__ void load_head(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint64_t start,
+                                          uint32_t (&h)[6])
+{
+    const uint64_t first = start & ~15ull;
+    uint32_t w[12];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const uint64_t o = first + 16 * c;
+        uint4 x;
+        if constexpr (BUF) {  // past the descriptor: zeros
+            const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<uint32_t>(o), 0, 0);
+            x = make_uint4(y.x, y.y, y.z, y.w);
+        } else {  // a chunk holding no arena byte is not read
+            const bool in = o < a.arena_bytes;
+            x = *reinterpret_cast<const uint4 *>(a.arena + (in ? o : first));
+        }
+        w[4 * c] = x.x;
+        w[4 * c + 1] = x.y;
+        w[4 * c + 2] = x.z;
+        w[4 * c + 3] = x.w;
+    }
+    const uint32_t q = static_cast<uint32_t>(start & 15) >> 2;
+    const uint32_t sh = static_cast<uint32_t>(start & 3);
+    uint32_t d[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+        d[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        h[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+}
+
+// h = the datagram's first 24 bytes (load_head), L = its length (the buffer length,
+// as the stack sees it).
+__device__ __forceinline__ RxParse rx_parse(const uint32_t (&h)[6], uint32_t L, uint32_t local4_sum,
+                                            uint32_t local6_sum)
 {
     RxParse r{kMetaMalformed, 0u, 0u};
     if (L == 0)
         return r;
-    const uint32_t version = p[0] >> 4;                      // ip.rs:40
+    auto p = [&](int i) -> uint32_t { return (h[i >> 2] >> (8 * (i & 3))) & 0xffu; };
+    const uint32_t version = p(0) >> 4;                      // ip.rs:40
     uint32_t proto = 0, src_sum = 0;
     bool v4src = false;
     if (version == 4) {
-        r.hdr = (p[0] & 0xf) * 4u;                           // ip.rs:71
+        r.hdr = (p(0) & 0xf) * 4u;                           // ip.rs:71
         if (r.hdr == 0 || L < 16 || r.hdr > L)               // empty slice / header index / trim_head panic
             return r;
         r.meta = kMetaV4;
-        if (((static_cast<uint32_t>(p[6]) << 8 | p[7]) & 0x3fff) != 0)  // ip.rs:84-87
+        if (((p(6) << 8 | p(7)) & 0x3fff) != 0)  // ip.rs:84-87
             r.meta |= kMetaFrag;
-        proto = p[9];                                        // ip.rs:89
-        src_sum = (static_cast<uint32_t>(p[12]) << 8 | p[13]) + (static_cast<uint32_t>(p[14]) << 8 | p[15]);
+        proto = p(9);                                        // ip.rs:89
+        src_sum = (p(12) << 8 | p(13)) + (p(14) << 8 | p(15));
         v4src = true;
     } else if (version == 6) {
         r.hdr = 40;
         if (L < 40)                                          // trim_head(IPV6_HEADER_LEN) would panic
             return r;
         r.meta = kMetaV6;
-        proto = p[6];                                        // ip.rs:110
+        proto = p(6);                                        // ip.rs:110
         for (int k = 8; k < 24; k += 2)                      // source address, ip.rs:111
-            src_sum += static_cast<uint32_t>(p[k]) << 8 | p[k + 1];
+            src_sum += p(k) << 8 | p(k + 1);
     } else {
         return r;                                            // "IP: Invalid version field"
     }
@@ -719,59 +817,93 @@ __device__ __forceinline__ uint8_t rx_verdict(uint32_t m, uint32_t hdr_res, uint
     return static_cast<uint8_t>(st);
 }
 
+// One packet's descriptor.  Loads are branch-free (an index past the batch re-reads
+// its last packet and the result is discarded), so no wait is forced at a branch merge.
+// With a buffer descriptor (arena < 4 GiB) the offset is held in 32 bits: one past
+// 4 GiB becomes 0xFFFFFFFF, still outside the arena, so it is still rejected.
+template <bool BUF>
+struct Desc {
+    typename std::conditional<BUF, uint32_t, uint64_t>::type off;
+    uint32_t len, field;
+};
+
+template <bool STRIDED, bool FILL, bool BUF>
+__device__ __forceinline__ Desc<BUF> load_desc(const CsumArgs &a, uint64_t p)
+{
+    const bool live = p < a.n;
+    const uint64_t q = live ? p : a.n - 1;
+    uint64_t off;
+    Desc<BUF> d;
+    if constexpr (STRIDED) {
+        off = a.first_off + q * a.stride;
+        d.len = a.fixed_len;
+    } else {
+        off = a.off[q];
+        d.len = a.len[q];
+    }
+    if constexpr (BUF)
+        d.off = off > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(off);
+    else
+        d.off = off;
+    d.field = FILL ? (a.field ? static_cast<uint32_t>(a.field[q]) : a.field_off) : 0xFFFFFFFFu;
+    d.off = live ? d.off : 0;
+    d.len = live ? d.len : 0u;
+    return d;
+}
+
 // FILL (transmit in-place fill, tcp.rs:957-973 / udp.rs:158-171 / icmp.rs:87-112 /
 // ip.rs:158-159): the 2-byte checksum field of each packet counts as zero while
 // summing, and the owner lane stores the (complemented) result into it, big-endian
 // (set_be16, util.rs:132-135), after the whole wave has read its 64 packets.
 template <bool STRIDED, bool NT, bool BUF, bool FILL, bool RX = false>
-__global__ __launch_bounds__(kBlock, (BUF && !FILL && !RX) ? 4 : 3) void csum_mixed_kernel(const CsumArgs a)
+#ifndef RNS_MIXED_OCC
+#define RNS_MIXED_OCC 4
+#endif
+__global__ __launch_bounds__(kBlock, (BUF && !FILL && !RX) ? RNS_MIXED_OCC : 3) void csum_mixed_kernel(const CsumArgs a)
 {
     static_assert(!(FILL && RX) && !(STRIDED && RX), "one mode at a time");
-    constexpr uint32_t kPer = RX ? 32 : 64;  // packets per wave batch (RX: two ranges per datagram)
+    constexpr uint32_t kPer = 64;  // packets per wave batch
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
 
-    for (uint64_t base = static_cast<uint64_t>(wave) * kPer; base < a.n; base += static_cast<uint64_t>(nwaves) * kPer) {
-        const uint64_t p = base + (RX ? (lane & 31) : lane);
+    // (Loading the descriptors one wave batch ahead was measured slower: the extra
+    // live registers spill at 4 waves/SIMD and the spill forces a wait on the loads.)
+    const uint64_t wstep = static_cast<uint64_t>(nwaves) * kPer;
+
+    for (uint64_t base = static_cast<uint64_t>(wave) * kPer; base < a.n; base += wstep) {
+        const uint64_t p = base + lane;
         const bool live = p < a.n;
-        uint64_t d_start = 0;
-        uint32_t d_len = 0, d_seed = 0;
-        if (live) {
-            if constexpr (STRIDED) {
-                d_start = a.first_off + p * a.stride;
-                d_len = a.fixed_len;
-            } else {
-                d_start = a.off[p];
-                d_len = a.len[p];
-            }
-            d_seed = a.seed ? a.seed[p] : 0u;
-        }
-        d_start += a.base_adjust;
-        uint32_t d_field = 0xFFFFFFFFu;
+        const Desc<BUF> cd = load_desc<STRIDED, FILL, BUF>(a, p);
+        uint64_t d_start = cd.off + a.base_adjust;
+        // the seed is first needed after the data pass: loaded here, its latency is hidden
+        uint32_t d_len = cd.len, d_seed = (a.seed && live) ? a.seed[p] : 0u;
+        uint32_t d_field = cd.field;  // FILL: the field offset; RX: the header length (split)
         bool d_ok = d_start <= a.arena_bytes && d_len <= a.arena_bytes - d_start;
         uint32_t rx_meta = 0;
-        if constexpr (RX) {  // this lane's range: lane < 32 the IPv4 header, lane >= 32 the L4 segment
-            const RxParse rp = (live && d_ok) ? rx_parse(a.arena + d_start, d_len, a.local4_sum, a.local6_sum)
-                                              : RxParse{kMetaMalformed, 0u, 0u};
+        if constexpr (RX) {  // this datagram's range and split (see above)
+            uint32_t head[6];
+            const bool parse = live && d_ok && d_len != 0;
+            load_head<BUF>(a, rsrc, parse ? d_start : 0u, head);  // unconditional: no divergent loads
+            const RxParse rp = parse ? rx_parse(head, d_len, a.local4_sum, a.local6_sum)
+                                     : RxParse{kMetaMalformed, 0u, 0u};
             rx_meta = rp.meta;
             const bool good = !(rp.meta & kMetaMalformed);
-            if (lane < 32) {
-                const bool v4 = good && (rp.meta & kMetaV4);
-                d_len = v4 ? rp.hdr : 0u;
-                d_seed = v4 ? 0u : 0xffffu;  // nothing to check: complemented result 0
+            const bool checked = good && (rp.meta & kMetaL4Checked);
+            if (good && (rp.meta & kMetaV4)) {
+                d_len = checked ? d_len : rp.hdr;
+                d_field = rp.hdr;
             } else {
-                const bool l4 = good && (rp.meta & kMetaL4Checked);
-                d_start += rp.hdr;
-                d_len = l4 ? d_len - rp.hdr : 0u;
-                d_seed = l4 ? rp.ph : 0xffffu;
+                d_start += checked ? rp.hdr : 0u;
+                d_len = checked ? d_len - rp.hdr : 0u;
+                d_field = 0u;
             }
+            d_seed = rp.ph;
             d_ok = true;
         }
         if constexpr (FILL) {
-            d_field = live ? (a.field ? static_cast<uint32_t>(a.field[p]) : a.field_off) : 0u;
             d_ok = d_ok && d_len >= 2 && d_field <= d_len - 2;  // header[f..f+2] must exist
             // (stores happen after the wave read all 64 packets: a store between a
             // prefetch and its consumer would serialise the in-order vmcnt waits)
@@ -781,6 +913,7 @@ __global__ __launch_bounds__(kBlock, (BUF && !FILL && !RX) ? 4 : 3) void csum_mi
             d_len = 0;
             d_start = 0;
         }
+        const bool odd = d_start & 1, big = d_len > kNoWrapBytes;  // all finalize needs of (start, len)
         // size class of this lane's packet; ranks within the class; sorted position
         const uint32_t nch = d_len ? static_cast<uint32_t>(((d_start & 15) + d_len + 15) >> 4) : 0u;
         uint32_t cls = kNumClasses - 1;
@@ -815,28 +948,36 @@ __global__ __launch_bounds__(kBlock, (BUF && !FILL && !RX) ? 4 : 3) void csum_mi
             __builtin_amdgcn_ds_permute(addr, static_cast<int>(static_cast<uint32_t>(d_start >> 32))));
         const uint32_t s_len = static_cast<uint32_t>(__builtin_amdgcn_ds_permute(addr, static_cast<int>(d_len)));
         const uint64_t s_start = (static_cast<uint64_t>(s_hi) << 32) | s_lo;
-        const uint32_t s_field =
-            FILL ? static_cast<uint32_t>(__builtin_amdgcn_ds_permute(addr, static_cast<int>(d_field))) : 0u;
+        const uint32_t s_aux = (FILL || RX)
+            ? static_cast<uint32_t>(__builtin_amdgcn_ds_permute(addr, static_cast<int>(d_field))) : 0u;
 
-        uint32_t mine = 0;
+        uint32_t mine = 0, mine_hdr = 0;
         uint4 v[kUMax];
-        Pkt cur = prefetch_class<NT, BUF, FILL>(a, rsrc, next[0], cr, s_start, s_len, s_field, lane, v);
-        run_class<0, NT, BUF, FILL>(a, rsrc, cr, next[1], s_start, s_len, s_field, cls == 0, rank, lane, cur, v, mine);
-        run_class<1, NT, BUF, FILL>(a, rsrc, cr, next[2], s_start, s_len, s_field, cls == 1, rank, lane, cur, v, mine);
-        run_class<2, NT, BUF, FILL>(a, rsrc, cr, next[3], s_start, s_len, s_field, cls == 2, rank, lane, cur, v, mine);
-        run_class<3, NT, BUF, FILL>(a, rsrc, cr, next[4], s_start, s_len, s_field, cls == 3, rank, lane, cur, v, mine);
-        run_class<4, NT, BUF, FILL>(a, rsrc, cr, next[5], s_start, s_len, s_field, cls == 4, rank, lane, cur, v, mine);
+        Pkt cur = prefetch_class<NT, BUF, FILL, RX>(a, rsrc, next[0], cr, s_start, s_len, s_aux, lane, v);
+#define RNS_RUN_CLASS(C)                                                                                      \
+        run_class<C, NT, BUF, FILL, RX>(a, rsrc, cr, next[C + 1], s_start, s_len, s_aux, cls == C, rank, lane, \
+                                        cur, v, mine, mine_hdr)
+        RNS_RUN_CLASS(0);
+        RNS_RUN_CLASS(1);
+        RNS_RUN_CLASS(2);
+        RNS_RUN_CLASS(3);
+        RNS_RUN_CLASS(4);
+#undef RNS_RUN_CLASS
 
-        const uint16_t res = finalize(mine, d_start, d_len, d_seed, d_ok, a.flags);
         if constexpr (RX) {
-            const uint32_t l4_res = static_cast<uint32_t>(__shfl(static_cast<int>(res), static_cast<int>((lane & 31) + 32), 64));
-            if (lane < 32 && live) {
-                a.status[p] = rx_verdict(rx_meta, res, l4_res);
+            // header: seed 0, LE sum (<= 60 bytes); L4: seed = pseudo-header sum.  Both
+            // parts start at the datagram's parity (the split is even).
+            const uint32_t hdr_res = finalize_bits(mine_hdr, odd, false, 0u, true, RNS_FLAG_COMPLEMENT);
+            const bool checked = rx_meta & kMetaL4Checked;
+            const uint32_t l4_res = checked ? finalize_bits(mine, odd, big, d_seed, true, RNS_FLAG_COMPLEMENT) : 0u;
+            if (live) {
+                a.status[p] = rx_verdict(rx_meta, hdr_res, l4_res);
                 if (a.l4_out)
                     a.l4_out[p] = static_cast<uint16_t>(l4_res);
             }
             continue;
         }
+        const uint16_t res = finalize_bits(mine, odd, big, d_seed, d_ok, a.flags);
         if (live && a.out)
             a.out[p] = res;  // 64 consecutive u16: one 128-byte store
         if constexpr (FILL) {
@@ -1266,13 +1407,18 @@ int rns_rx_verify_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64
     a.l4_out = d_l4_sum;
     a.local4_sum = be_sum(local_ipv4, 4);
     a.local6_sum = be_sum(local_ipv6, 16);
-    const uint64_t waves = (static_cast<uint64_t>(n) + 31) / 32;  // 32 datagrams per wave
+    const uint64_t waves = (static_cast<uint64_t>(n) + 63) / 64;  // 64 datagrams per wave
     const dim3 grid(static_cast<uint32_t>((waves + kBlock / 64 - 1) / (kBlock / 64))), block(kBlock);
     hipStream_t st = static_cast<hipStream_t>(stream);
+#ifdef RNS_RX_PLAIN
+    constexpr bool kNT = false;
+#else
+    constexpr bool kNT = true;
+#endif
     if (buf_records(a) < kOobOffset)
-        hipLaunchKernelGGL((csum_mixed_kernel<false, true, true, false, true>), grid, block, 0, st, a);
+        hipLaunchKernelGGL((csum_mixed_kernel<false, kNT, true, false, true>), grid, block, 0, st, a);
     else
-        hipLaunchKernelGGL((csum_mixed_kernel<false, true, false, false, true>), grid, block, 0, st, a);
+        hipLaunchKernelGGL((csum_mixed_kernel<false, kNT, false, false, true>), grid, block, 0, st, a);
     return hip_status(hipGetLastError());
 }
 
@@ -1409,6 +1555,131 @@ int rns_csum_batch_host(rns_host_ctx *ctx, const uint8_t *h_arena, uint64_t aren
         if (st == RNS_OK)
             st = d;
     }
+    return st;
+}
+
+// ---------------------------------------------------------------------------
+// Multi-GPU batches: packets are independent, so a batch
+// is cut into contiguous packet ranges of about equal BYTES, one per GPU; each GPU
+// checksums its range from its own HBM (device-resident) or through its own
+// staging context and PCIe link (host-resident).  No bytes cross xGMI and no
+// collective is needed: each range's results land in their slice of h_out.
+// ---------------------------------------------------------------------------
+struct rns_multi_ctx {
+    std::vector<rns_host_ctx *> ctx;
+};
+
+int rns_multi_ctx_create(const int *devices, uint32_t ndev, uint64_t chunk_bytes, uint32_t nstreams,
+                         rns_multi_ctx **out)
+{
+    if (!out || !devices || ndev == 0 || ndev > 64)
+        return RNS_E_INVALID;
+    *out = nullptr;
+    rns_multi_ctx *m = new (std::nothrow) rns_multi_ctx;
+    if (!m)
+        return RNS_E_INVALID;
+    for (uint32_t i = 0; i < ndev; ++i) {
+        rns_host_ctx *c = nullptr;
+        const int st = rns_host_ctx_create(devices[i], chunk_bytes, nstreams, &c);
+        if (st) {
+            rns_multi_ctx_destroy(m);
+            return st;
+        }
+        m->ctx.push_back(c);
+    }
+    *out = m;
+    return RNS_OK;
+}
+
+int rns_multi_ctx_destroy(rns_multi_ctx *ctx)
+{
+    if (ctx) {
+        for (rns_host_ctx *c : ctx->ctx)
+            rns_host_ctx_destroy(c);
+        delete ctx;
+    }
+    return RNS_OK;
+}
+
+extern "C++" {
+namespace {
+// Cut [0, n) into `parts` contiguous ranges of about equal byte totals: bounds[0..parts].
+std::vector<uint32_t> split_by_bytes(const uint32_t *len, uint32_t n, uint32_t parts)
+{
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        total += len[i];
+    std::vector<uint32_t> bounds(parts + 1, n);
+    bounds[0] = 0;
+    uint64_t acc = 0;
+    uint32_t i = 0;
+    for (uint32_t k = 1; k < parts; ++k) {
+        const uint64_t target = total * k / parts;
+        while (i < n && acc + len[i] <= target)
+            acc += len[i++];
+        bounds[k] = std::max(i, bounds[k - 1]);
+    }
+    return bounds;
+}
+}  // namespace
+}  // extern "C++"
+
+int rns_csum_batch_multi_host(rns_multi_ctx *ctx, const uint8_t *h_arena, uint64_t arena_bytes,
+                              const uint64_t *h_off, const uint32_t *h_len, const uint16_t *h_seed,
+                              uint16_t *h_out, uint32_t n, uint32_t flags)
+{
+    if (!ctx || ctx->ctx.empty())
+        return RNS_E_INVALID;
+    if (n == 0)
+        return RNS_OK;
+    if (!h_arena || !h_off || !h_len || !h_out)
+        return RNS_E_INVALID;
+    const uint32_t parts = static_cast<uint32_t>(ctx->ctx.size());
+    const std::vector<uint32_t> b = split_by_bytes(h_len, n, parts);
+    std::vector<int> st(parts, RNS_OK);
+    auto run = [&](uint32_t k) {
+        const uint32_t i0 = b[k], cnt = b[k + 1] - b[k];
+        if (cnt)
+            st[k] = rns_csum_batch_host(ctx->ctx[k], h_arena, arena_bytes, h_off + i0, h_len + i0,
+                                        h_seed ? h_seed + i0 : nullptr, h_out + i0, cnt, flags);
+    };
+    std::vector<std::thread> workers;
+    for (uint32_t k = 1; k < parts; ++k) {
+        try {
+            workers.emplace_back(run, k);
+        } catch (...) {
+            run(k);  // no thread available: run this range inline
+        }
+    }
+    run(0);
+    for (auto &w : workers)
+        w.join();
+    for (int x : st)
+        if (x)
+            return x;
+    return RNS_OK;
+}
+
+int rns_csum_batch_multi_dev(const rns_dev_batch *batches, uint32_t nbatches, uint32_t flags)
+{
+    if (nbatches == 0)
+        return RNS_OK;
+    if (!batches)
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess)
+        return RNS_E_NODEVICE;
+    int st = RNS_OK;
+    for (uint32_t k = 0; k < nbatches && st == RNS_OK; ++k) {  // launches are asynchronous: GPUs run together
+        const rns_dev_batch &d = batches[k];
+        st = hip_status(hipSetDevice(d.device));
+        if (st == RNS_OK)
+            st = rns_csum_batch_dev(d.d_arena, d.arena_bytes, d.d_off, d.d_len, d.d_seed, d.d_out, d.n, flags,
+                                    d.len_hint, d.d_bad, d.stream);
+    }
+    (void)hipSetDevice(prev);
     return st;
 }
 

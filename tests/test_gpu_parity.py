@@ -21,6 +21,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 SHAPES = [(var, g, u) for var in (0, 1) for g in (4, 8, 16, 32, 64) for u in (1, 2, 4, 8)]
 SHAPES += [(var, 64, 4) for var in (2, 3, 4, 6)]
+SHAPES += [(var, 2, u) for var in (1, 3) for u in (1, 2, 4)]  # 2-lane groups: rounds kernel only
 
 
 def host_u16(t: torch.Tensor) -> np.ndarray:

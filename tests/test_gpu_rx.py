@@ -71,11 +71,67 @@ def test_mixed_datagrams_match_reference_path(oracle):
     arena, off, ln = pack(pkts, 0xBEEF)
     expect = np.array([O.rx_status_ref(p, L4, L6, ones_comp=oracle.compute_ones_comp) for p in pkts], dtype=np.uint8)
     assert len(set(expect.tolist())) >= 6          # every kind of verdict is exercised
-    st = rx_verify(torch.from_numpy(arena).to(DEV), dev(off, np.int64), dev(ln, np.int32), L4, L6)
+    l4 = torch.empty(len(pkts), dtype=torch.uint16, device=DEV)
+    st = rx_verify(torch.from_numpy(arena).to(DEV), dev(off, np.int64), dev(ln, np.int32), L4, L6, l4_sum=l4)
     torch.cuda.synchronize()
     got = st.cpu().numpy()
     bad = np.nonzero(got != expect)[0]
     assert bad.size == 0, [(int(i), int(got[i]), int(expect[i]), pkts[i][:24].hex()) for i in bad[:5]]
+    want_l4 = np.array([O.rx_verify_ref(p, L4, L6, ones_comp=oracle.compute_ones_comp)[1] for p in pkts],
+                       dtype=np.uint16)
+    got_l4 = l4.view(torch.int16).cpu().numpy().view(np.uint16)
+    bad = np.nonzero(got_l4 != want_l4)[0]
+    assert bad.size == 0, [(int(i), int(got_l4[i]), int(want_l4[i])) for i in bad[:5]]
+
+
+def jumbo_v4(proto, seg):
+    """IPv4 datagram longer than 64 KiB (the total-length field wraps; the stack uses
+    the buffer length, ip.rs:94-96)."""
+    h = bytearray(20)
+    h[0] = 0x45
+    h[2:4] = ((20 + len(seg)) & 0xFFFF).to_bytes(2, "big")
+    h[8], h[9] = 64, proto
+    h[12:16], h[16:20] = R4, L4
+    h[10:12] = O.checksum_py(bytes(h)).to_bytes(2, "big")
+    return bytes(h) + seg
+
+
+def test_edge_datagrams_match_reference_path(oracle):
+    """Datagrams the split header/L4 pass must get right: L4 segments past the
+    128 KiB no-wrap bound (exact big-endian path, the IP header still split off),
+    headers with options whose end falls anywhere in a 16-byte chunk, empty L4
+    segments, header-only UDP, and 0xff-filled bodies (maximal sums)."""
+    pkts = []
+    for k, size in enumerate((131_072 - 20, 131_072 + 7, 200_001, 262_144 + 3)):
+        body = O.splitmix64_bytes(0xB16 + k, size).tobytes()
+        seg = bytearray(tcp_seg(R4, L4, body))
+        pkts.append(jumbo_v4(6, bytes(seg)))
+        seg6 = tcp_seg(R6, L6, body)
+        pkts.append(ipv6(6, seg6) if len(seg6) < 65536 else
+                    bytes(bytearray([0x60, 0, 0, 0, 0, 0, 6, 64]) + R6 + L6) + seg6)
+        bad = bytearray(pkts[-2])
+        bad[len(bad) // 2] ^= 0x80
+        pkts.append(bytes(bad))
+    ff = b"\xff" * 70_000
+    pkts.append(jumbo_v4(1, icmp4(ff)))
+    for ihl in range(5, 16):
+        for size in (0, 1, 2, 3, 17, 31, 64):
+            pkts.append(ipv4(6, tcp_seg(R4, L4, b"\xa5" * size), ihl=ihl))
+        pkts.append(ipv4(6, b"", ihl=ihl))                 # empty TCP segment: L4 sum = seed
+        pkts.append(ipv4(17, b"", ihl=ihl))                # header-only UDP
+        pkts.append(ipv4(1, b"\x00", ihl=ihl))             # 1-byte ICMP
+    pkts.append(ipv6(6, b""))
+    pkts.append(ipv6(58, b"\x01"))
+    expect = [O.rx_verify_ref(p, L4, L6, ones_comp=oracle.compute_ones_comp) for p in pkts]
+    for shift in (0, 1, 0x11):
+        arena, off, ln = pack(pkts, 0x5A17 + shift)
+        off = off + shift
+        arena = np.concatenate([np.zeros(shift, dtype=np.uint8), arena])
+        l4 = torch.empty(len(pkts), dtype=torch.uint16, device=DEV)
+        st = rx_verify(torch.from_numpy(arena).to(DEV), dev(off, np.int64), dev(ln, np.int32), L4, L6, l4_sum=l4)
+        got = list(zip(st.cpu().numpy().tolist(), l4.view(torch.int16).cpu().numpy().view(np.uint16).tolist()))
+        bad = [(i, len(pkts[i]), got[i], expect[i]) for i in range(len(pkts)) if got[i] != tuple(expect[i])]
+        assert not bad, bad[:5]
 
 
 def test_full_size_tcp_batch_verifies_and_catches_corruption():

@@ -75,8 +75,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--configs", default="c3_1500B,c5_imix")
+    ap.add_argument("--ops", default="csum,chain,fill,verify")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
+    ops = set(args.ops.split(","))
     dev = torch.device("cuda:0")
     results = {}
     for cfg in args.configs.split(","):
@@ -86,48 +88,24 @@ def main():
         r = {}
         pb = PreparedBatch(b.arena, b.off, b.length, b.seed, complement=True, out=b.out,
                            len_hint=int(round(lay.mean_len)))
-        ms = timed(pb, args.steps, args.rounds)
-        r["csum"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1)}
-        # chain: three fragments per packet where the packet is long enough, else one
-        L = lay.length.astype(np.int64)
-        nfr = np.where(L > 1004, 3, 1)
-        first = np.zeros(n + 1, dtype=np.int64)
-        np.cumsum(nfr, out=first[1:])
-        nf = int(first[-1])
-        frag_off = np.empty(nf, dtype=np.uint64)
-        frag_len = np.empty(nf, dtype=np.uint32)
-        three = nfr == 3
-        i3 = first[:-1][three]
-        frag_off[i3] = lay.off[three]
-        frag_off[i3 + 1] = lay.off[three] + 492
-        frag_off[i3 + 2] = lay.off[three] + 1004
-        frag_len[i3] = 492
-        frag_len[i3 + 1] = 512
-        frag_len[i3 + 2] = (L[three] - 1004).astype(np.uint32)
-        i1 = first[:-1][~three]
-        frag_off[i1] = lay.off[~three]
-        frag_len[i1] = lay.length[~three]
-        d_fo = torch.from_numpy(frag_off.view(np.int64)).to(dev)
-        d_fl = torch.from_numpy(frag_len.view(np.int32)).to(dev)
-        d_first = torch.from_numpy(first.astype(np.uint32).view(np.int32)).to(dev)
-        sums = torch.empty(nf, dtype=torch.uint16, device=dev)
-        out = torch.empty(n, dtype=torch.uint16, device=dev)
-        ms = timed(lambda: csum_chain(b.arena, d_fo, d_fl, d_first, b.seed, complement=True, out=out,
-                                      frag_sums=sums, frag_len_hint=int(round(pay / nf))),
-                   args.steps, args.rounds)
-        r["chain"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1),
-                      "fragments": nf}
-        ms = timed(lambda: csum_fill(b.arena, b.off, b.length, b.seed, field_off=16), args.steps, args.rounds)
-        r["fill"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1)}
-        # verify: turn every packet into a valid IPv4/TCP datagram first (header written
-        # on the GPU, IPv4 and TCP checksums filled), so every byte is checked
-        write_ipv4_tcp_headers(b, lay, dev)
-        st = torch.empty(n, dtype=torch.uint8, device=dev)
-        ms = timed(lambda: rx_verify(b.arena, b.off, b.length, L4, L6, status=st),
-                   args.steps, args.rounds)
-        accepted = int((st == 0x43).sum().item())
-        r["verify"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + n) / ms / 1e6, 1),
-                       "accepted": accepted, "packets": n}
+        if "csum" in ops:
+            ms = timed(pb, args.steps, args.rounds)
+            r["csum"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1)}
+        if "chain" in ops:
+            r["chain"] = bench_chain(b, lay, dev, args)
+        if "fill" in ops:
+            ms = timed(lambda: csum_fill(b.arena, b.off, b.length, b.seed, field_off=16), args.steps, args.rounds)
+            r["fill"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1)}
+        if "verify" in ops:
+            # turn every packet into a valid IPv4/TCP datagram first (header written
+            # on the GPU, IPv4 and TCP checksums filled), so every byte is checked
+            write_ipv4_tcp_headers(b, lay, dev)
+            st = torch.empty(n, dtype=torch.uint8, device=dev)
+            ms = timed(lambda: rx_verify(b.arena, b.off, b.length, L4, L6, status=st),
+                       args.steps, args.rounds)
+            accepted = int((st == 0x43).sum().item())
+            r["verify"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + n) / ms / 1e6, 1),
+                           "accepted": accepted, "packets": n}
         results[cfg] = r
         print(cfg, json.dumps(r), flush=True)
         del b
@@ -137,6 +115,38 @@ def main():
             json.dump({"tool": "tools/bench_ops.py", "steps": args.steps, "rounds": args.rounds,
                        "results": results}, f, indent=1)
     print(json.dumps(results))
+
+
+def bench_chain(b, lay, dev, args):
+    n, pay = lay.n, lay.payload_bytes
+    # chain: three fragments per packet where the packet is long enough, else one
+    L = lay.length.astype(np.int64)
+    nfr = np.where(L > 1004, 3, 1)
+    first = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(nfr, out=first[1:])
+    nf = int(first[-1])
+    frag_off = np.empty(nf, dtype=np.uint64)
+    frag_len = np.empty(nf, dtype=np.uint32)
+    three = nfr == 3
+    i3 = first[:-1][three]
+    frag_off[i3] = lay.off[three]
+    frag_off[i3 + 1] = lay.off[three] + 492
+    frag_off[i3 + 2] = lay.off[three] + 1004
+    frag_len[i3] = 492
+    frag_len[i3 + 1] = 512
+    frag_len[i3 + 2] = (L[three] - 1004).astype(np.uint32)
+    i1 = first[:-1][~three]
+    frag_off[i1] = lay.off[~three]
+    frag_len[i1] = lay.length[~three]
+    d_fo = torch.from_numpy(frag_off.view(np.int64)).to(dev)
+    d_fl = torch.from_numpy(frag_len.view(np.int32)).to(dev)
+    d_first = torch.from_numpy(first.astype(np.uint32).view(np.int32)).to(dev)
+    sums = torch.empty(nf, dtype=torch.uint16, device=dev)
+    out = torch.empty(n, dtype=torch.uint16, device=dev)
+    ms = timed(lambda: csum_chain(b.arena, d_fo, d_fl, d_first, b.seed, complement=True, out=out,
+                                  frag_sums=sums, frag_len_hint=int(round(pay / nf))),
+               args.steps, args.rounds)
+    return {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1), "fragments": nf}
 
 
 if __name__ == "__main__":
