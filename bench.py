@@ -58,7 +58,14 @@ class Dist:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        # Rehearsal knobs (never set by the driver): RNS_BENCH_BACKEND=gloo and
+        # RNS_BENCH_DEVICE=0 run N ranks on ONE GPU to exercise the N>1 path.
+        if os.environ.get("RNS_BENCH_DEVICE") is not None:
+            self.local_rank = int(os.environ["RNS_BENCH_DEVICE"])
+        backend = backend or os.environ.get("RNS_BENCH_BACKEND") or None
         self.enabled = self.world > 1
+        if self.enabled and torch.cuda.is_available():
+            torch.cuda.set_device(self.local_rank)  # before RCCL binds its communicator
         if self.enabled and not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             dist.init_process_group(backend=backend or ("nccl" if torch.cuda.is_available() else "gloo"))
