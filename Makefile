@@ -29,11 +29,11 @@ $(LIB): $(BUILD)/rns_checksum.o $(BUILD)/host_checksum.o $(BUILD)/host_io.o
 oracle:
 	$(MAKE) -C oracle
 
-# A/B experiment build: `make ab ABDEF=-DRNS_TINY_G2 ABNAME=tinyg2` -> tools/ab/librns_checksum_tinyg2.so
-# (load it with RNS_CHECKSUM_LIB=...).  RNS_TINY_G2: tiny packets with 2 lanes each in
-# the mixed kernel; RNS_RX_PLAIN: receive verify with plain (temporal) loads.
-ABDEF  ?= -DRNS_TINY_G2
-ABNAME ?= tinyg2
+# A/B experiment build: `make ab ABDEF="-DRNS_CLASS_U=1,4,4,3,4" ABNAME=u3` -> tools/ab/librns_checksum_u3.so
+# (load it with RNS_CHECKSUM_LIB=...).  Knobs: RNS_CLASS_LOG2G / RNS_CLASS_U (mixed-kernel class shapes),
+# RNS_MIXED_OCC (waves/SIMD bound), RNS_FILL_BLOCK, RNS_FILL_NOSTORE, RNS_RX_PLAIN.
+ABDEF  ?= -DRNS_CLASS_U=1,4,4,3,4
+ABNAME ?= u3
 AB_LIB := tools/ab/librns_checksum_$(ABNAME).so
 $(AB_LIB): $(CSRC)/rns_checksum.hip $(BUILD)/host_checksum.o $(BUILD)/host_io.o include/rns_checksum.h
 	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) $(ABDEF) -Iinclude -c $< -o $(BUILD)/rns_checksum_$(ABNAME).o

@@ -243,44 +243,93 @@ constexpr uint32_t kOobOffset = 0xFFFFF000u;
 // bytes, and are masked away like every byte outside a packet).
 __host__ __device__ __forceinline__ uint64_t buf_records(const CsumArgs &a) { return (a.arena_bytes + 15) & ~15ull; }
 
+// Chunk stash (receive verify and transmit fill).  The word sum is linear in the
+// bytes, so verify and fill run the PLAIN data pass over the whole packet; the few
+// chunks their finish needs (a datagram's header, a packet's checksum field) are
+// copied to LDS by the lanes that load them anyway, and the owner lane finishes
+// from there: no extra memory round, no per-chunk header/field masking.
+enum StashMode : int { kStashNone = 0, kStashHead = 1, kStashField = 2 };
+// Chunks stashed per packet: a datagram's first 5 chunks hold its first
+// 16*5 - 15 = 65 >= 60 bytes (the longest IPv4 header) at any start offset; a
+// field's chunks are the 32-byte sector that holds its first byte plus the next
+// chunk (a field at the sector's last byte spills into it).
+#ifndef RNS_FILL_BLOCK
+#define RNS_FILL_BLOCK 32
+#endif
+// Transmit fill rewrites the largest aligned block (kFieldBlock, /2, ... 32 bytes)
+// around the field that lies inside the packet; the stash holds that block's chunks
+// plus the next one.
+constexpr int kFieldBlock = RNS_FILL_BLOCK;
+constexpr int kFieldChunks = kFieldBlock / 16;
+static_assert(kFieldBlock >= 32 && kFieldBlock <= 128 && (kFieldBlock & (kFieldBlock - 1)) == 0, "fill block");
+template <int MODE>
+constexpr int kStashChunks = MODE == kStashHead ? 5 : MODE == kStashField ? kFieldChunks + 1 : 0;
+
+// First stashed chunk (relative to the packet's chunk 0) for a field whose first
+// byte is in chunk cf: the chunk that starts the field's aligned kFieldBlock-byte
+// block in MEMORY (chunk0 = the packet's chunk 0 index from the 16-byte aligned
+// arena base; apar = that base's chunk index mod kFieldChunks).  May be negative.
+__host__ __device__ __forceinline__ int field_block_lo(uint32_t cf, uint32_t chunk0, uint32_t apar)
+{
+    return static_cast<int>(cf) - static_cast<int>((apar + chunk0 + cf) & (kFieldChunks - 1));
+}
+
 struct Pkt {
     uint64_t start;       // packet byte offset from the 16-byte aligned arena base
     uint32_t nch;         // 16-byte chunks covering the packet (0 if empty)
     int s;                // first valid byte in chunk 0
     int e;                // bytes valid in the last chunk (1..16)
     bool big;             // > kNoWrapBytes: exact big-endian path
-    int hole;             // transmit fill: the 2-byte checksum field, as a byte index from
-                          // chunk 0's first byte (counted as zero while summing); kNoHole: none
-    int split;            // receive verify: bytes before this index (from chunk 0's first byte)
-                          // are the IP header and go to a separate sum; == s: no header bytes
+    int stash_lo;         // stash: first chunk to copy to LDS
+    int stash_at;         // stash: LDS chunk index of that chunk's slot
 };
 
-constexpr int kNoHole = -4096;
-
-__device__ __forceinline__ Pkt make_pkt(uint64_t start, uint32_t L, uint32_t field = 0xFFFFFFFFu,
-                                        uint32_t split = 0u)
+__device__ __forceinline__ Pkt make_pkt(uint64_t start, uint32_t L)
 {
     Pkt k;
     k.start = start;
-    k.hole = (field < L) ? static_cast<int>(start & 15) + static_cast<int>(field) : kNoHole;
     k.s = static_cast<int>(k.start & 15);
-    k.split = k.s + static_cast<int>(min(split, 4096u));
     const uint64_t span = static_cast<uint64_t>(k.s) + L;
     k.nch = L ? static_cast<uint32_t>((span + 15) >> 4) : 0u;
     k.e = static_cast<int>(span - (static_cast<uint64_t>(k.nch ? k.nch - 1 : 0) << 4));
     k.big = L > kNoWrapBytes;
+    k.stash_lo = 0;
+    k.stash_at = 0;
     return k;
 }
 
-// d_aux: the hole's field offset (HOLE) or the header length (SPLIT).
-template <int G, bool HOLE = false, bool SPLIT = false>
-__device__ __forceinline__ Pkt fetch_pkt(uint64_t d_start, uint32_t d_len, uint32_t src, uint32_t d_aux = 0xFFFFFFFFu)
+// Stash slots of the packet at sorted position `slot`.  kStashField: `field` = its
+// checksum field offset; the stash starts at the chunk that begins the field's
+// 32-byte MEMORY sector (apar = parity of the arena base's 16-byte chunk index), so
+// slots 0-1 are that sector whenever it lies inside the packet.
+template <int MODE>
+__device__ __forceinline__ void set_stash(Pkt &k, uint32_t slot, uint32_t field, uint32_t apar)
+{
+    if constexpr (MODE != kStashNone) {
+        k.stash_at = static_cast<int>(slot) * kStashChunks<MODE>;
+        if constexpr (MODE == kStashField) {
+            const uint32_t cf = (static_cast<uint32_t>(k.s) + min(field, 1u << 30)) >> 4;
+            k.stash_lo = field_block_lo(cf, static_cast<uint32_t>(k.start >> 4), apar);
+        }
+    }
+}
+
+template <int G, int MODE = kStashNone>
+__device__ __forceinline__ Pkt fetch_pkt(uint64_t d_start, uint32_t d_len, uint32_t src, uint32_t d_aux = 0xFFFFFFFFu,
+                                         uint32_t apar = 0)
 {
     const uint32_t lo = bcast_from<G>(static_cast<uint32_t>(d_start), src);
     const uint32_t hi = bcast_from<G>(static_cast<uint32_t>(d_start >> 32), src);
     const uint32_t L = bcast_from<G>(d_len, src);
-    const uint32_t x = (HOLE || SPLIT) ? bcast_from<G>(d_aux, src) : 0xFFFFFFFFu;
-    return make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L, HOLE ? x : 0xFFFFFFFFu, SPLIT ? x : 0u);
+    const uint32_t x = MODE == kStashField ? bcast_from<G>(d_aux, src) : 0xFFFFFFFFu;
+    Pkt k = make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L);
+    set_stash<MODE>(k, src, x, apar);
+    return k;
+}
+
+__device__ __forceinline__ uint32_t arena_parity(const CsumArgs &a)
+{
+    return static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a.arena) >> 4) & (kFieldChunks - 1);
 }
 
 // Loads of one pass: chunk c = c0 + u*G of the packet, for u < U.  Branch-free:
@@ -309,17 +358,7 @@ __device__ __forceinline__ void issue_pass(const CsumArgs &a, __amdgpu_buffer_rs
     }
 }
 
-// Zero bytes [lo, hi) of the 4-byte dword at byte j4 of a 16-byte chunk.
-__device__ __forceinline__ uint32_t drop_bytes(uint32_t d, int lo, int hi, int j4)
-{
-    const int a = min(max(lo - j4, 0), 4);
-    const int b = min(max(hi - j4, 0), 4);
-    const uint32_t hm = static_cast<uint32_t>((1ull << (8 * b)) - 1);
-    const uint32_t lm = static_cast<uint32_t>((1ull << (8 * a)) - 1);
-    return d & ~(hm & ~lm);
-}
-
-template <int G, int U, int N = U, bool HOLE = false>
+template <int G, int U, int N = U>
 __device__ __forceinline__ void mask_edges(const Pkt &k, uint32_t c0, uint4 (&v)[N])
 {
 #pragma unroll
@@ -333,14 +372,23 @@ __device__ __forceinline__ void mask_edges(const Pkt &k, uint32_t c0, uint4 (&v)
             v[u].z = keep_bytes(v[u].z, lo, hi, 8);
             v[u].w = keep_bytes(v[u].w, lo, hi, 12);
         }
-        if constexpr (HOLE) {  // the checksum field counts as zero (alloc_header zero-fills it, buf.rs:286-288)
-            const int hp = k.hole - 16 * static_cast<int>(c);
-            if (hp > -2 && hp < 16) {
-                v[u].x = drop_bytes(v[u].x, hp, hp + 2, 0);
-                v[u].y = drop_bytes(v[u].y, hp, hp + 2, 4);
-                v[u].z = drop_bytes(v[u].z, hp, hp + 2, 8);
-                v[u].w = drop_bytes(v[u].w, hp, hp + 2, 12);
-            }
+    }
+}
+
+// Copy the chunks of this pass that the finish needs to their LDS slots (after
+// edge masking: only bytes outside the packet were zeroed, and the finish reads
+// none of those).  Chunks past the packet's end are never written: their slot may
+// belong to a valid packet of another group.
+template <int MODE, int G, int U, int N = U>
+__device__ __forceinline__ void stash_chunks(const Pkt &k, uint32_t c0, const uint4 (&v)[N], uint4 *st)
+{
+    if constexpr (MODE != kStashNone) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + u * G;
+            const uint32_t i = c - static_cast<uint32_t>(k.stash_lo);
+            if (i < static_cast<uint32_t>(kStashChunks<MODE>) && c < k.nch)
+                st[k.stash_at + static_cast<int>(i)] = v[u];
         }
     }
 }
@@ -377,44 +425,21 @@ __device__ __forceinline__ void sum_be(const uint4 (&v)[N], uint32_t w_hi, uint3
     }
 }
 
-// Receive verify: move the IP-header bytes of each chunk (index < k.split) out of
-// v into the header's own LE sum.  Only the first few chunks of a datagram hold
-// header bytes (IHL*4 <= 60), so the branch is rarely taken.
-template <int G, int U, int N = U>
-__device__ __forceinline__ void split_header(const Pkt &k, uint32_t c0, uint4 (&v)[N], uint32_t &hdr)
-{
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int b = k.split - 16 * static_cast<int>(c0 + u * G);  // header bytes in this chunk
-        if (b > 0) {
-            const uint4 h = make_uint4(keep_bytes(v[u].x, 0, b, 0), keep_bytes(v[u].y, 0, b, 4),
-                                       keep_bytes(v[u].z, 0, b, 8), keep_bytes(v[u].w, 0, b, 12));
-            hdr = __builtin_amdgcn_sad_u16(h.x, 0, hdr);
-            hdr = __builtin_amdgcn_sad_u16(h.y, 0, hdr);
-            hdr = __builtin_amdgcn_sad_u16(h.z, 0, hdr);
-            hdr = __builtin_amdgcn_sad_u16(h.w, 0, hdr);
-            v[u] = make_uint4(v[u].x ^ h.x, v[u].y ^ h.y, v[u].z ^ h.z, v[u].w ^ h.w);
-        }
-    }
-}
-
 // One packet's contribution from this lane.  `v` holds the (prefetched) first pass.
-// SPLIT: the bytes before k.split are summed into `hdr` (LE) instead.
-template <int G, int U, bool NT, bool BUF, int N = U, bool HOLE = false, bool SPLIT = false>
+// MODE != kStashNone: the chunks the finish needs are also copied to LDS (`st`).
+template <int G, int U, bool NT, bool BUF, int N = U, int MODE = kStashNone>
 __device__ __forceinline__ uint32_t packet_partial(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, const Pkt &k,
-                                                   uint32_t sub, uint4 (&v)[N], uint32_t &hdr)
+                                                   uint32_t sub, uint4 (&v)[N], uint4 *st = nullptr)
 {
     constexpr uint32_t kPass = G * U;
-    mask_edges<G, U, N, HOLE>(k, sub, v);
-    if constexpr (SPLIT)
-        split_header<G, U, N>(k, sub, v, hdr);
+    mask_edges<G, U, N>(k, sub, v);
+    stash_chunks<MODE, G, U, N>(k, sub, v, st);
     if (!k.big) {
         uint32_t acc = sum_le<U, N>(v, 0u);
         for (uint32_t c0 = kPass + sub; c0 < k.nch; c0 += kPass) {  // packets longer than one pass (reuse v)
             issue_pass<G, U, NT, BUF, N>(a, rsrc, k, c0, v);
-            mask_edges<G, U, N, HOLE>(k, c0, v);
-            if constexpr (SPLIT)
-                split_header<G, U, N>(k, c0, v, hdr);
+            mask_edges<G, U, N>(k, c0, v);
+            stash_chunks<MODE, G, U, N>(k, c0, v, st);
             acc = sum_le<U, N>(v, acc);
         }
         return acc;  // LE-word sum, exact (< 2^32 for a packet of <= 128 KiB)
@@ -424,9 +449,8 @@ __device__ __forceinline__ uint32_t packet_partial(const CsumArgs &a, __amdgpu_b
     sum_be<U, N>(v, w_hi, hs, ls);
     for (uint32_t c0 = kPass + sub; c0 < k.nch; c0 += kPass) {
         issue_pass<G, U, NT, BUF, N>(a, rsrc, k, c0, v);
-        mask_edges<G, U, N, HOLE>(k, c0, v);
-        if constexpr (SPLIT)
-            split_header<G, U, N>(k, c0, v, hdr);
+        mask_edges<G, U, N>(k, c0, v);
+        stash_chunks<MODE, G, U, N>(k, c0, v, st);
         sum_be<U, N>(v, w_hi, hs, ls);
     }
     return (hs << 8) + ls;  // BE-word sum mod 2^32, exactly the reference's accumulator
@@ -514,8 +538,7 @@ __global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
             nxt.nch = has_next ? nxt.nch : 0u;
             uint4 w[U];
             issue_pass<G, U, NT, BUF>(a, rsrc, nxt, sub, w);
-            uint32_t unused = 0;
-            const uint32_t words = group_allreduce<G>(packet_partial<G, U, NT, BUF>(a, rsrc, cur, sub, v, unused));
+            const uint32_t words = group_allreduce<G>(packet_partial<G, U, NT, BUF>(a, rsrc, cur, sub, v));
             if constexpr (G == 64) {
                 mine = (lane == r) ? words : mine;
             } else {
@@ -555,19 +578,21 @@ struct ClassRun {
 // Size classes (16-byte chunks a packet spans) and the shape each class runs with.
 constexpr uint32_t kNumClasses = 5;
 constexpr uint32_t kClassMax[kNumClasses - 1] = {4, 16, 64, 128};  // above the last: jumbo
-#ifdef RNS_TINY_G2
-constexpr uint32_t kClassLog2G[kNumClasses] = {1, 2, 4, 5, 6};     // lanes per packet 2, 4, 16, 32, 64
-constexpr uint32_t kClassU[kNumClasses] = {2, 4, 4, 4, 4};         // chunks in flight per lane
-#else
-constexpr uint32_t kClassLog2G[kNumClasses] = {2, 2, 4, 5, 6};     // lanes per packet 4, 4, 16, 32, 64
-constexpr uint32_t kClassU[kNumClasses] = {1, 4, 4, 4, 4};         // chunks in flight per lane
+// (A/B builds override these: -DRNS_CLASS_LOG2G=1,2,4,5,6 -DRNS_CLASS_U=2,4,4,4,4)
+#ifndef RNS_CLASS_LOG2G
+#define RNS_CLASS_LOG2G 2, 2, 4, 5, 6
 #endif
+#ifndef RNS_CLASS_U
+#define RNS_CLASS_U 1, 4, 4, 4, 4
+#endif
+constexpr uint32_t kClassLog2G[kNumClasses] = {RNS_CLASS_LOG2G};   // lanes per packet 4, 4, 16, 32, 64
+constexpr uint32_t kClassU[kNumClasses] = {RNS_CLASS_U};           // chunks in flight per lane
 constexpr int kUMax = 4;
 
 // Round 0 of class n (wave-uniform; kNumClasses = none), issued with the class's
 // runtime shape into the shared buffer: the last round of the previous class
 // calls this, so a class starts with its first pass already in flight.
-template <bool NT, bool BUF, bool FILL, bool RX>
+template <bool NT, bool BUF, int MODE>
 __device__ __forceinline__ Pkt prefetch_class(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint32_t n,
                                               const ClassRun (&cr)[kNumClasses], uint64_t s_start, uint32_t s_len,
                                               uint32_t s_aux, uint32_t lane, uint4 (&w)[kUMax])
@@ -589,8 +614,9 @@ __device__ __forceinline__ Pkt prefetch_class(const CsumArgs &a, __amdgpu_buffer
     const uint32_t lo = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(s_start)), src, 64));
     const uint32_t hi = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(s_start >> 32)), src, 64));
     const uint32_t L = static_cast<uint32_t>(__shfl(static_cast<int>(s_len), src, 64));
-    const uint32_t x = (FILL || RX) ? static_cast<uint32_t>(__shfl(static_cast<int>(s_aux), src, 64)) : 0xFFFFFFFFu;
-    Pkt k = make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L, FILL ? x : 0xFFFFFFFFu, RX ? x : 0u);
+    const uint32_t x = MODE == kStashField ? static_cast<uint32_t>(__shfl(static_cast<int>(s_aux), src, 64)) : 0xFFFFFFFFu;
+    Pkt k = make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L);
+    set_stash<MODE>(k, static_cast<uint32_t>(src), x, arena_parity(a));
     k.nch = valid ? k.nch : 0u;
     const uint64_t first = k.start - static_cast<uint64_t>(k.s);
 #pragma unroll
@@ -611,12 +637,11 @@ __device__ __forceinline__ Pkt prefetch_class(const CsumArgs &a, __amdgpu_buffer
 
 // All rounds of class C.  On entry (cur, v) hold round 0's prefetched first pass;
 // on exit they hold the first pass of class `next` (the next non-empty class).
-template <uint32_t C, bool NT, bool BUF, bool FILL, bool RX>
+template <uint32_t C, bool NT, bool BUF, int MODE>
 __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc,
                                           const ClassRun (&cr)[kNumClasses], uint32_t next, uint64_t s_start,
                                           uint32_t s_len, uint32_t s_aux, bool in_class, uint32_t rank,
-                                          uint32_t lane, Pkt &cur, uint4 (&v)[kUMax], uint32_t &mine,
-                                          uint32_t &mine_hdr)
+                                          uint32_t lane, Pkt &cur, uint4 (&v)[kUMax], uint32_t &mine, uint4 *st)
 {
     constexpr int G = 1 << kClassLog2G[C];
     constexpr int U = static_cast<int>(kClassU[C]);
@@ -628,28 +653,19 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
         return;  // (cur, v) already hold the next class's prefetch
     auto fetch = [&](uint32_t r) {  // group `grp` of round r: sorted position off + r*P + grp
         const uint32_t i = r * P + grp;
-        Pkt k = fetch_pkt<G, FILL, RX>(s_start, s_len, cr[C].off + (i < cr[C].cnt ? i : 0), s_aux);
+        Pkt k = fetch_pkt<G, MODE>(s_start, s_len, cr[C].off + (i < cr[C].cnt ? i : 0), s_aux, arena_parity(a));
         k.nch = (i < cr[C].cnt) ? k.nch : 0u;
         return k;
     };
     auto finish = [&](uint32_t r) {  // consume round r from (cur, v), route each sum to its owner lane
-        uint32_t hdr = 0;
         const uint32_t words =
-            group_allreduce<G>(packet_partial<G, U, NT, BUF, kUMax, FILL, RX>(a, rsrc, cur, sub, v, hdr));
-        if constexpr (RX)
-            hdr = group_allreduce<G>(hdr);
+            group_allreduce<G>(packet_partial<G, U, NT, BUF, kUMax, MODE>(a, rsrc, cur, sub, v, st));
         if constexpr (G == 64) {
             mine = (in_class && rank == r) ? words : mine;  // wave-uniform sum
-            if constexpr (RX)
-                mine_hdr = (in_class && rank == r) ? hdr : mine_hdr;
         } else {
             const int src = static_cast<int>((rank % P) * G);
             const uint32_t t = static_cast<uint32_t>(__shfl(static_cast<int>(words), src, 64));
             mine = (in_class && rank / P == r) ? t : mine;
-            if constexpr (RX) {
-                const uint32_t th = static_cast<uint32_t>(__shfl(static_cast<int>(hdr), src, 64));
-                mine_hdr = (in_class && rank / P == r) ? th : mine_hdr;
-            }
         }
     };
     for (uint32_t r = 0; r + 1 < rounds; ++r) {
@@ -663,7 +679,7 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
             v[u] = w[u];
     }
     uint4 w[kUMax];
-    const Pkt nxt = prefetch_class<NT, BUF, FILL, RX>(a, rsrc, next, cr, s_start, s_len, s_aux, lane, w);
+    const Pkt nxt = prefetch_class<NT, BUF, MODE>(a, rsrc, next, cr, s_start, s_len, s_aux, lane, w);
     finish(rounds - 1);
     cur = nxt;
 #pragma unroll
@@ -672,19 +688,18 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
 }
 
 // ---------------------------------------------------------------------------
-// Receive verify (§8f row 1), fused into the mixed kernel (RX = true): the checks
+// Receive verify (§8f row 1), fused into the mixed kernel (kStashHead): the checks
 // ip_input_v4 (ip.rs:65-92), ip_input_v6 (ip.rs:108-115), ip_input_common
 // (ip.rs:117-128), tcp::validate_checksum (tcp.rs:838-850), icmp_input_v4
 // (icmp.rs:44-50) and icmp_input_v6 (icmp.rs:62-75) apply to a received datagram.
-// A wave takes 64 datagrams, one per owner lane, which parses its header (a few byte
-// loads of lines the data pass reads next) and turns it into ONE byte range and a
-// split point: IPv4 with a checked L4 -> the whole datagram, split at IHL*4; IPv4
-// otherwise -> the header alone; IPv6 with a checked L4 -> the L4 segment (no header
-// checksum in IPv6).  The data pass sums the bytes before the split (the header) and
-// after it (the L4 segment, seeded with the pseudo-header sum: dest = the LOCAL
-// address, as the reference passes netif::get_ipaddr()) separately, and the owner
-// lane combines both.  The split is even (IHL*4 or 40), so both parts pair their
-// bytes exactly as the reference's separate calls do.
+// A wave takes 64 datagrams, one per owner lane.  The data pass is the plain one
+// over the WHOLE datagram (its LE word sum T); the lanes that load a datagram's
+// first 5 chunks also copy them to LDS.  The owner lane then parses the header from
+// LDS and sums the header bytes H itself (<= 60 bytes), so the L4 segment's sum is
+// T - H: the word sum is linear in the bytes, and the header length (IHL*4 or 40) is
+// even, so the L4 bytes pair exactly as the reference's separate call over the
+// trimmed packet pairs them.  The L4 seed is the pseudo-header sum with dest = the
+// LOCAL address, as the reference passes netif::get_ipaddr().
 // ---------------------------------------------------------------------------
 enum : uint32_t {
     kMetaV4 = 1, kMetaV6 = 2, kMetaFrag = 4, kMetaMalformed = 8,
@@ -705,33 +720,12 @@ struct RxParse {
 };
 
 // The first 24 bytes of a datagram (every field rx_parse reads) as six dwords in
-// datagram byte order, from the three aligned 16-byte chunks around them, all
-// loaded at once (one memory latency, where per-field byte loads took two
-// dependent ones).  Bytes past the datagram are not used: rx_parse checks L first.
-template <bool BUF>
-__device__ __forceinline__ void load_head(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint64_t start,
-                                          uint32_t (&h)[6])
+// datagram byte order, from the stashed chunks 0..2 (s = start & 15).
+__device__ __forceinline__ void head_from_stash(const uint4 (&ch)[5], uint32_t s, uint32_t (&h)[6])
 {
-    const uint64_t first = start & ~15ull;
-    uint32_t w[12];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const uint64_t o = first + 16 * c;
-        uint4 x;
-        if constexpr (BUF) {  // past the descriptor: zeros
-            const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<uint32_t>(o), 0, 0);
-            x = make_uint4(y.x, y.y, y.z, y.w);
-        } else {  // a chunk holding no arena byte is not read
-            const bool in = o < a.arena_bytes;
-            x = *reinterpret_cast<const uint4 *>(a.arena + (in ? o : first));
-        }
-        w[4 * c] = x.x;
-        w[4 * c + 1] = x.y;
-        w[4 * c + 2] = x.z;
-        w[4 * c + 3] = x.w;
-    }
-    const uint32_t q = static_cast<uint32_t>(start & 15) >> 2;
-    const uint32_t sh = static_cast<uint32_t>(start & 3);
+    const uint32_t w[12] = {ch[0].x, ch[0].y, ch[0].z, ch[0].w, ch[1].x, ch[1].y,
+                            ch[1].z, ch[1].w, ch[2].x, ch[2].y, ch[2].z, ch[2].w};
+    const uint32_t q = s >> 2, sh = s & 3;
     uint32_t d[7];
 #pragma unroll
     for (int k = 0; k < 7; ++k)
@@ -741,7 +735,39 @@ __device__ __forceinline__ void load_head(const CsumArgs &a, __amdgpu_buffer_rsr
         h[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
 }
 
-// h = the datagram's first 24 bytes (load_head), L = its length (the buffer length,
+// Word sums of bytes [lo, hi) of the stashed chunks (byte index from chunk 0's
+// first byte; hi <= 80): LE words at aligned positions (v_sad_u16), or the exact
+// big-endian words relative to a packet start of parity `odd` (256*hi + lo bytes).
+template <int NCH>
+__device__ __forceinline__ uint32_t stash_sum_le(const uint4 (&ch)[NCH], int lo, int hi)
+{
+    uint32_t acc = 0;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        acc = __builtin_amdgcn_sad_u16(keep_bytes(ch[c].x, lo - 16 * c, hi - 16 * c, 0), 0, acc);
+        acc = __builtin_amdgcn_sad_u16(keep_bytes(ch[c].y, lo - 16 * c, hi - 16 * c, 4), 0, acc);
+        acc = __builtin_amdgcn_sad_u16(keep_bytes(ch[c].z, lo - 16 * c, hi - 16 * c, 8), 0, acc);
+        acc = __builtin_amdgcn_sad_u16(keep_bytes(ch[c].w, lo - 16 * c, hi - 16 * c, 12), 0, acc);
+    }
+    return acc;
+}
+
+template <int NCH>
+__device__ __forceinline__ uint32_t stash_sum_be(const uint4 (&ch)[NCH], int lo, int hi, bool odd)
+{
+    uint4 m[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+        m[c] = make_uint4(keep_bytes(ch[c].x, lo - 16 * c, hi - 16 * c, 0),
+                          keep_bytes(ch[c].y, lo - 16 * c, hi - 16 * c, 4),
+                          keep_bytes(ch[c].z, lo - 16 * c, hi - 16 * c, 8),
+                          keep_bytes(ch[c].w, lo - 16 * c, hi - 16 * c, 12));
+    uint32_t hs = 0, ls = 0;
+    sum_be<NCH, NCH>(m, odd ? 0x01000100u : 0x00010001u, hs, ls);
+    return (hs << 8) + ls;
+}
+
+// h = the datagram's first 24 bytes (head_from_stash), L = its length (the buffer length,
 // as the stack sees it).
 __device__ __forceinline__ RxParse rx_parse(const uint32_t (&h)[6], uint32_t L, uint32_t local4_sum,
                                             uint32_t local6_sum)
@@ -852,9 +878,12 @@ __device__ __forceinline__ Desc<BUF> load_desc(const CsumArgs &a, uint64_t p)
 }
 
 // FILL (transmit in-place fill, tcp.rs:957-973 / udp.rs:158-171 / icmp.rs:87-112 /
-// ip.rs:158-159): the 2-byte checksum field of each packet counts as zero while
-// summing, and the owner lane stores the (complemented) result into it, big-endian
-// (set_be16, util.rs:132-135), after the whole wave has read its 64 packets.
+// ip.rs:158-159): the checksum is that of the packet with its 2-byte field zeroed
+// (alloc_header zero-fills it, buf.rs:286-288).  The data pass sums the whole packet;
+// the owner lane subtracts the field's word contribution (its bytes from the stash),
+// folds, and stores the (complemented) result into the field big-endian (set_be16,
+// util.rs:132-135) after the whole wave has read its 64 packets.
+// RX: receive verify (see above).
 template <bool STRIDED, bool NT, bool BUF, bool FILL, bool RX = false>
 #ifndef RNS_MIXED_OCC
 #define RNS_MIXED_OCC 4
@@ -862,7 +891,12 @@ template <bool STRIDED, bool NT, bool BUF, bool FILL, bool RX = false>
 __global__ __launch_bounds__(kBlock, (BUF && !FILL && !RX) ? RNS_MIXED_OCC : 3) void csum_mixed_kernel(const CsumArgs a)
 {
     static_assert(!(FILL && RX) && !(STRIDED && RX), "one mode at a time");
+    constexpr int kMode = RX ? kStashHead : FILL ? kStashField : kStashNone;
+    constexpr int kNS = kStashChunks<kMode>;
     constexpr uint32_t kPer = 64;  // packets per wave batch
+    // per wave: kNS chunks for each of its 64 packets, indexed by sorted position
+    __shared__ uint4 stash_lds[kNS ? (kBlock / 64) * kPer * kNS : 1];
+    uint4 *const st = stash_lds + (threadIdx.x >> 6) * (kPer * kNS);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
@@ -879,36 +913,15 @@ __global__ __launch_bounds__(kBlock, (BUF && !FILL && !RX) ? RNS_MIXED_OCC : 3) 
         const Desc<BUF> cd = load_desc<STRIDED, FILL, BUF>(a, p);
         uint64_t d_start = cd.off + a.base_adjust;
         // the seed is first needed after the data pass: loaded here, its latency is hidden
-        uint32_t d_len = cd.len, d_seed = (a.seed && live) ? a.seed[p] : 0u;
-        uint32_t d_field = cd.field;  // FILL: the field offset; RX: the header length (split)
+        uint32_t d_len = cd.len;
+        const uint32_t d_seed = (a.seed && live) ? a.seed[p] : 0u;
+        const uint32_t d_field = cd.field;  // FILL: the field offset
         bool d_ok = d_start <= a.arena_bytes && d_len <= a.arena_bytes - d_start;
-        uint32_t rx_meta = 0;
-        if constexpr (RX) {  // this datagram's range and split (see above)
-            uint32_t head[6];
-            const bool parse = live && d_ok && d_len != 0;
-            load_head<BUF>(a, rsrc, parse ? d_start : 0u, head);  // unconditional: no divergent loads
-            const RxParse rp = parse ? rx_parse(head, d_len, a.local4_sum, a.local6_sum)
-                                     : RxParse{kMetaMalformed, 0u, 0u};
-            rx_meta = rp.meta;
-            const bool good = !(rp.meta & kMetaMalformed);
-            const bool checked = good && (rp.meta & kMetaL4Checked);
-            if (good && (rp.meta & kMetaV4)) {
-                d_len = checked ? d_len : rp.hdr;
-                d_field = rp.hdr;
-            } else {
-                d_start += checked ? rp.hdr : 0u;
-                d_len = checked ? d_len - rp.hdr : 0u;
-                d_field = 0u;
-            }
-            d_seed = rp.ph;
-            d_ok = true;
-        }
         if constexpr (FILL) {
             d_ok = d_ok && d_len >= 2 && d_field <= d_len - 2;  // header[f..f+2] must exist
             // (stores happen after the wave read all 64 packets: a store between a
             // prefetch and its consumer would serialise the in-order vmcnt waits)
         }
-        const uint64_t own_start = d_start;
         if (!d_ok || d_len == 0) {
             d_len = 0;
             d_start = 0;
@@ -948,15 +961,15 @@ __global__ __launch_bounds__(kBlock, (BUF && !FILL && !RX) ? RNS_MIXED_OCC : 3) 
             __builtin_amdgcn_ds_permute(addr, static_cast<int>(static_cast<uint32_t>(d_start >> 32))));
         const uint32_t s_len = static_cast<uint32_t>(__builtin_amdgcn_ds_permute(addr, static_cast<int>(d_len)));
         const uint64_t s_start = (static_cast<uint64_t>(s_hi) << 32) | s_lo;
-        const uint32_t s_aux = (FILL || RX)
+        const uint32_t s_aux = FILL
             ? static_cast<uint32_t>(__builtin_amdgcn_ds_permute(addr, static_cast<int>(d_field))) : 0u;
 
-        uint32_t mine = 0, mine_hdr = 0;
+        uint32_t mine = 0;
         uint4 v[kUMax];
-        Pkt cur = prefetch_class<NT, BUF, FILL, RX>(a, rsrc, next[0], cr, s_start, s_len, s_aux, lane, v);
-#define RNS_RUN_CLASS(C)                                                                                      \
-        run_class<C, NT, BUF, FILL, RX>(a, rsrc, cr, next[C + 1], s_start, s_len, s_aux, cls == C, rank, lane, \
-                                        cur, v, mine, mine_hdr)
+        Pkt cur = prefetch_class<NT, BUF, kMode>(a, rsrc, next[0], cr, s_start, s_len, s_aux, lane, v);
+#define RNS_RUN_CLASS(C)                                                                                   \
+        run_class<C, NT, BUF, kMode>(a, rsrc, cr, next[C + 1], s_start, s_len, s_aux, cls == C, rank, lane, \
+                                     cur, v, mine, st)
         RNS_RUN_CLASS(0);
         RNS_RUN_CLASS(1);
         RNS_RUN_CLASS(2);
@@ -965,52 +978,93 @@ __global__ __launch_bounds__(kBlock, (BUF && !FILL && !RX) ? RNS_MIXED_OCC : 3) 
 #undef RNS_RUN_CLASS
 
         if constexpr (RX) {
-            // header: seed 0, LE sum (<= 60 bytes); L4: seed = pseudo-header sum.  Both
-            // parts start at the datagram's parity (the split is even).
-            const uint32_t hdr_res = finalize_bits(mine_hdr, odd, false, 0u, true, RNS_FLAG_COMPLEMENT);
-            const bool checked = rx_meta & kMetaL4Checked;
-            const uint32_t l4_res = checked ? finalize_bits(mine, odd, big, d_seed, true, RNS_FLAG_COMPLEMENT) : 0u;
+            // mine = the whole datagram's word sum T.  Header H from the stash (seed 0,
+            // <= 60 bytes); L4 = T - H, seeded with the pseudo-header sum.  Both parts
+            // start at the datagram's parity (the header length is even).
+            uint4 ch[kNS];
+#pragma unroll
+            for (int i = 0; i < kNS; ++i)
+                ch[i] = st[pos * kNS + i];
+            const uint32_t s = static_cast<uint32_t>(d_start & 15);
+            uint32_t head[6];
+            head_from_stash(ch, s, head);
+            const RxParse rp = (live && d_len != 0) ? rx_parse(head, d_len, a.local4_sum, a.local6_sum)
+                                                    : RxParse{kMetaMalformed, 0u, 0u};
+            uint32_t hdr_res = 0, l4_res = 0;
+            if (!(rp.meta & kMetaMalformed)) {
+                const int hlo = static_cast<int>(s), hhi = hlo + static_cast<int>(rp.hdr);  // <= 15 + 60
+                const uint32_t H = stash_sum_le(ch, hlo, hhi);
+                hdr_res = finalize_bits(H, odd, false, 0u, true, RNS_FLAG_COMPLEMENT);
+                if (rp.meta & kMetaL4Checked) {
+                    const uint32_t l4 = big ? mine - stash_sum_be(ch, hlo, hhi, odd) : mine - H;
+                    l4_res = finalize_bits(l4, odd, big, rp.ph, true, RNS_FLAG_COMPLEMENT);
+                }
+            }
             if (live) {
-                a.status[p] = rx_verdict(rx_meta, hdr_res, l4_res);
+                a.status[p] = rx_verdict(rp.meta, hdr_res, l4_res);
                 if (a.l4_out)
                     a.l4_out[p] = static_cast<uint16_t>(l4_res);
             }
             continue;
         }
+        uint64_t blk = 0;      // FILL: offset (from a.arena) of the stashed block around the field
+        uint32_t f_rel = 0;    // FILL: the field's first byte in that block (0 .. kFieldBlock-1)
+        uint32_t w_size = 0;   // FILL: bytes of the largest aligned block inside the packet (0: none)
+        if constexpr (FILL) {  // take the field's bytes out of the sum: it counts as zero
+            const uint32_t s = static_cast<uint32_t>(d_start & 15);
+            const uint32_t fpos = s + d_field;                       // from chunk 0's first byte
+            const int lo = field_block_lo(fpos >> 4, static_cast<uint32_t>(d_start >> 4), arena_parity(a));
+            f_rel = fpos - 16u * static_cast<uint32_t>(lo);
+            blk = d_start - s + static_cast<uint64_t>(16 * static_cast<int64_t>(lo));
+            const uint8_t *sb = reinterpret_cast<const uint8_t *>(st + pos * kNS);
+            const uint32_t b0 = d_ok ? sb[f_rel] : 0u, b1 = d_ok ? sb[f_rel + 1] : 0u;
+            // LE words pair aligned bytes; the exact BE path pairs from the packet start
+            const bool hi_first = big ? !(d_field & 1) : (fpos & 1);
+            mine -= hi_first ? (b0 << 8) + b1 : b0 + (b1 << 8);
+#pragma unroll
+            for (uint32_t bs = 32; bs <= static_cast<uint32_t>(kFieldBlock); bs *= 2) {
+                const uint64_t b = blk + (f_rel & ~(bs - 1));       // the bs-byte block holding the field
+                const bool in = lo >= 0 && b >= d_start && b + bs <= d_start + d_len && (f_rel & (bs - 1)) != bs - 1;
+                w_size = in ? bs : w_size;
+            }
+        }
         const uint16_t res = finalize_bits(mine, odd, big, d_seed, d_ok, a.flags);
         if (live && a.out)
             a.out[p] = res;  // 64 consecutive u16: one 128-byte store
         if constexpr (FILL) {
+#ifndef RNS_FILL_NOSTORE
             if (live && d_ok) {  // set_be16(&mut header[f..f+2], checksum)
                 uint8_t *arena_w = const_cast<uint8_t *>(a.arena);
-                const uint64_t fpos = own_start + d_field;       // field offset from the aligned arena
-                const uint64_t sec = fpos & ~31ull;              // its 32-byte memory sector
                 const uint32_t be = (res >> 8) | ((res & 0xffu) << 8);
-                if (sec >= own_start && sec + 32 <= own_start + d_len && (fpos & 31) != 31) {
-                    // The whole sector belongs to this packet (packets never overlap), so
-                    // rewrite it entirely: a full-sector write needs no read-modify-write
-                    // at the memory side, unlike a 2-byte masked store.
-                    uint4 *sp = reinterpret_cast<uint4 *>(arena_w + sec);
-                    uint4 lo = sp[0], hi = sp[1];
-                    uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-                    const uint32_t b = static_cast<uint32_t>(fpos & 31);
+                if (w_size) {
+                    // The whole block belongs to this packet (packets never overlap) and its
+                    // bytes are in the stash: rewrite it entirely, since a full-sector write
+                    // needs no read-modify-write at the memory side.
+                    const uint32_t c_lo = (f_rel & ~(w_size - 1)) >> 4, c_hi = c_lo + (w_size >> 4);
 #pragma unroll
-                    for (uint32_t k = 0; k < 2; ++k) {  // bytes b and b+1 (same or adjacent dword)
-                        const uint32_t pos = b + k, di = pos >> 2, sh = (pos & 3) * 8;
-                        const uint32_t byte = (be >> (8 * k)) & 0xffu;
+                    for (uint32_t i = 0; i < static_cast<uint32_t>(kFieldChunks); ++i) {
+                        if (i >= c_lo && i < c_hi) {
+                            const uint4 c = st[pos * kNS + i];
+                            uint32_t w[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
-                        for (uint32_t d = 0; d < 8; ++d)
-                            if (d == di)
-                                w[d] = (w[d] & ~(0xffu << sh)) | (byte << sh);
+                            for (uint32_t k = 0; k < 2; ++k) {  // bytes f_rel and f_rel+1
+                                const uint32_t bpos = f_rel + k - 16 * i, sh = (bpos & 3) * 8;
+                                const uint32_t byte = (be >> (8 * k)) & 0xffu;
+#pragma unroll
+                                for (uint32_t d = 0; d < 4; ++d)
+                                    if (bpos < 16 && d == (bpos >> 2))
+                                        w[d] = (w[d] & ~(0xffu << sh)) | (byte << sh);
+                            }
+                            *reinterpret_cast<uint4 *>(arena_w + blk + 16 * i) = make_uint4(w[0], w[1], w[2], w[3]);
+                        }
                     }
-                    sp[0] = make_uint4(w[0], w[1], w[2], w[3]);
-                    sp[1] = make_uint4(w[4], w[5], w[6], w[7]);
                 } else {
-                    uint8_t *q = arena_w + fpos;
+                    uint8_t *q = arena_w + d_start + d_field;
                     q[0] = static_cast<uint8_t>(res >> 8);
                     q[1] = static_cast<uint8_t>(res);
                 }
             }
+#endif
         }
         if (a.bad) {
             const uint64_t rejected = __ballot(live && !d_ok);

@@ -1,0 +1,188 @@
+// Scattered-store probe for MI355X: what does the transmit fill's one small store per
+// packet cost, alone and fused behind a streaming read of the packets?
+//
+//   hipcc --offload-arch=gfx950 -O3 tools/store_probe.hip -o tools/store_probe
+//   ./tools/store_probe [packets] [stride]
+//
+// Packets of `stride` bytes back to back (default 2^20 x 1504 B, the c3 arena); the
+// "field" is at byte 16 of each packet.  Variants:
+//   scatter{2,16,32,64}  one lane per packet stores N bytes at the field (aligned block)
+//   read                 one wave per 64 packets streams their bytes (16 B/lane, 4 in flight)
+//   read+store{2,32}     the same, then each lane stores into one packet's field
+//   read+compact         the same, then one coalesced 128-B store of 64 u16 results
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CHECK(x)                                                                              \
+    do {                                                                                      \
+        hipError_t e_ = (x);                                                                  \
+        if (e_ != hipSuccess) {                                                               \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));    \
+            std::exit(1);                                                                     \
+        }                                                                                     \
+    } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int B>
+__global__ __launch_bounds__(256) void scatter(uint8_t *arena, uint32_t n, uint32_t stride, uint32_t v)
+{
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint64_t f = static_cast<uint64_t>(i) * stride + 16;
+    if constexpr (B == 2) {
+        *reinterpret_cast<uint16_t *>(arena + f) = static_cast<uint16_t>(v);
+    } else {
+        uint4 *q = reinterpret_cast<uint4 *>(arena + (f & ~static_cast<uint64_t>(B - 1)));
+#pragma unroll
+        for (int k = 0; k < B / 16; ++k)
+            q[k] = make_uint4(v, v + k, v, v);
+    }
+}
+
+// MODE 0: read only; 1: + 2-byte field store; 2: + 32-byte sector store; 3: + compact u16 store
+// at the end of the wave's slab.  MODE 4: the lane that loaded a packet's field chunk
+// rewrites that 16-B chunk right after consuming it; MODE 5: the same store issued one
+// iteration later, after the next iteration's loads (so no load waits for it).
+// CACHE: buffer-load cache policy bits (0 = default, 2 = nontemporal).
+template <int MODE, int CACHE = 2>
+__global__ __launch_bounds__(256) void read_store(uint8_t *arena, uint32_t n, uint32_t stride, uint16_t *out)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
+    const uint64_t p0 = static_cast<uint64_t>(wave) * 64;
+    if (p0 >= n)
+        return;
+    const uint32_t np = min(64u, n - static_cast<uint32_t>(p0));
+    const uint64_t b0 = p0 * stride, nch = (static_cast<uint64_t>(np) * stride) >> 4;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(arena + b0, 0, static_cast<int>(nch * 16), 0x00020000);
+    const uint32_t fch = 16 / 16, sch = stride / 16;  // the field's chunk within a packet; chunks per packet
+    uint32_t acc = 0;
+    bool pend = false;
+    uint64_t pc = 0;
+    u32x4 pv = {0, 0, 0, 0};
+    for (uint64_t c = lane; c < nch; c += 256) {
+        u32x4 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            x[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<uint32_t>((c + 64 * u) * 16), 0, CACHE);
+        if constexpr (MODE == 5) {
+            if (pend)
+                *reinterpret_cast<u32x4 *>(arena + b0 + pc * 16) = pv;
+            pend = false;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            acc = __builtin_amdgcn_sad_u16(x[u].x, 0, acc);
+            acc = __builtin_amdgcn_sad_u16(x[u].y, 0, acc);
+            acc = __builtin_amdgcn_sad_u16(x[u].z, 0, acc);
+            acc = __builtin_amdgcn_sad_u16(x[u].w, 0, acc);
+            if constexpr (MODE == 4 || MODE == 5) {
+                const uint64_t cc = c + 64 * u;
+                if (cc < nch && cc % sch == fch) {
+                    u32x4 y = x[u];
+                    y.x = acc;
+                    if constexpr (MODE == 4) {
+                        *reinterpret_cast<u32x4 *>(arena + b0 + cc * 16) = y;
+                    } else {
+                        pend = true;
+                        pc = cc;
+                        pv = y;
+                    }
+                }
+            }
+        }
+    }
+    if constexpr (MODE == 5) {
+        if (pend)
+            *reinterpret_cast<u32x4 *>(arena + b0 + pc * 16) = pv;
+    }
+    if constexpr (MODE >= 4)
+        return;
+    if (lane >= np)
+        return;
+    const uint64_t f = (p0 + lane) * stride + 16;
+    if constexpr (MODE == 0) {
+        if (acc == 0x12345678u)
+            out[p0 + lane] = 1;
+    } else if constexpr (MODE == 1) {
+        *reinterpret_cast<uint16_t *>(arena + f) = static_cast<uint16_t>(acc);
+    } else if constexpr (MODE == 2) {
+        uint4 *q = reinterpret_cast<uint4 *>(arena + (f & ~31ull));
+        q[0] = make_uint4(acc, acc, acc, acc);
+        q[1] = make_uint4(acc, 0, acc, 0);
+    } else {
+        out[p0 + lane] = static_cast<uint16_t>(acc);
+    }
+}
+
+template <class F>
+static float time_ms(F launch, int iters)
+{
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    launch();
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(a));
+    for (int i = 0; i < iters; ++i)
+        launch();
+    CHECK(hipEventRecord(b));
+    CHECK(hipEventSynchronize(b));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    return ms / iters;
+}
+
+int main(int argc, char **argv)
+{
+    const uint32_t n = argc > 1 ? static_cast<uint32_t>(std::strtoul(argv[1], nullptr, 0)) : (1u << 20);
+    const uint32_t stride = argc > 2 ? static_cast<uint32_t>(std::strtoul(argv[2], nullptr, 0)) : 1504u;
+    if (stride % 32 != 0 && stride % 16 != 0) {
+        std::fprintf(stderr, "stride must be a multiple of 16\n");
+        return 1;
+    }
+    const uint64_t bytes = static_cast<uint64_t>(n) * stride;
+    uint8_t *arena;
+    uint16_t *out;
+    CHECK(hipMalloc(&arena, bytes + 256));
+    CHECK(hipMalloc(&out, static_cast<size_t>(n) * 2));
+    CHECK(hipMemset(arena, 0x5a, bytes));
+    const int iters = 20;
+    const uint32_t sblocks = (n + 255) / 256, rblocks = (n + 255) / 256;  // read: 4 waves of 64 packets per block
+    std::printf("{\"packets\": %u, \"stride\": %u, \"bytes\": %llu, \"results\": [\n", n, stride,
+                static_cast<unsigned long long>(bytes));
+    bool first = true;
+    auto report = [&](const char *name, float ms) {
+        std::printf("%s{\"variant\": \"%s\", \"us\": %.1f, \"read_GBps\": %.1f}\n", first ? "" : ",", name, ms * 1e3,
+                    bytes / (ms * 1e-3) / 1e9);
+        first = false;
+    };
+    for (int rep = 0; rep < 2; ++rep) {
+        report("scatter2", time_ms([&] { scatter<2><<<sblocks, 256>>>(arena, n, stride, 7); }, iters));
+        report("scatter16", time_ms([&] { scatter<16><<<sblocks, 256>>>(arena, n, stride, 7); }, iters));
+        report("scatter32", time_ms([&] { scatter<32><<<sblocks, 256>>>(arena, n, stride, 7); }, iters));
+        report("scatter64", time_ms([&] { scatter<64><<<sblocks, 256>>>(arena, n, stride, 7); }, iters));
+        report("read", time_ms([&] { read_store<0><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read+store2", time_ms([&] { read_store<1><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read+store32", time_ms([&] { read_store<2><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read+compact", time_ms([&] { read_store<3><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read+inline16", time_ms([&] { read_store<4><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read+deferred16", time_ms([&] { read_store<5><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read_plain", time_ms([&] { read_store<0, 0><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read_plain+store32", time_ms([&] { read_store<2, 0><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read_plain+inline16", time_ms([&] { read_store<4, 0><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read_plain+deferred16", time_ms([&] { read_store<5, 0><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read;scatter32", time_ms([&] {
+                   read_store<3><<<rblocks, 256>>>(arena, n, stride, out);
+                   scatter<32><<<sblocks, 256>>>(arena, n, stride, 7);
+               }, iters));
+    }
+    std::printf("]}\n");
+    CHECK(hipFree(arena));
+    CHECK(hipFree(out));
+    return 0;
+}
