@@ -43,6 +43,10 @@ def parse_args(argv=None):
     p.add_argument("--gather", action="store_true",
                    help="add an RCCL all_gather of every rank's results to each step (not the default: "
                         "the stack consumes results where they are produced)")
+    p.add_argument("--scaling", choices=("auto", "weak", "strong"), default="auto",
+                   help="weak: every rank checksums a full batch of the config; strong: the config's batch is "
+                        "sharded by packet index across ranks (auto: strong for c5_imix, whose BASELINE.json "
+                        "config is one 8M-packet batch over 8 GPUs; weak otherwise)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_{config}.json"))
     return p.parse_args(argv)
 
@@ -79,13 +83,19 @@ class Dist:
             else:
                 self.dist.barrier()
 
-    def max(self, x: float) -> float:
+    def _reduce(self, x: float, op) -> float:
         if not self.enabled:
             return x
         dev = f"cuda:{self.local_rank}" if self.backend == "nccl" else "cpu"
         t = self.torch.tensor([x], dtype=self.torch.float64, device=dev)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(t, op=op)
         return float(t.item())
+
+    def max(self, x: float) -> float:
+        return self._reduce(x, self.dist.ReduceOp.MAX)
+
+    def sum(self, x: float) -> float:
+        return self._reduce(x, self.dist.ReduceOp.SUM)
 
     def close(self):
         if self.enabled and self.dist.is_initialized():
@@ -120,20 +130,27 @@ def timed_loop(engine, dist: Dist, steps: int, warmup: int) -> dict:
 # ---------------------------------------------------------------------------
 class GpuEngine:
     def __init__(self, config: str, rank: int, local_rank: int, shape=None, gather_dist: Dist | None = None,
-                 steps: int = 0):
+                 steps: int = 0, world: int = 1, strong: bool = False):
         import torch
 
         from rustnetworkstack_amd.workloads import DATA_SEED, DeviceBatch, make_layout
         self.torch = torch
         self.device = torch.device(f"cuda:{local_rank}")
         torch.cuda.set_device(self.device)
-        # weak scaling: every rank owns a full batch of the config, with its own bytes
-        self.layout = make_layout(config, data_seed=DATA_SEED + 0x1000 * rank)
+
+        def layout(r):
+            if strong:  # this rank's packet-index shard of the one batch (same sizes and seeds on every rank)
+                lay = make_layout(config, shard=(rank, world))
+                lay.data_seed = DATA_SEED + 0x1000 * rank + r
+                return lay
+            # weak scaling: every rank owns a full batch of the config, with its own bytes
+            return make_layout(config, data_seed=DATA_SEED + 0x1000 * rank + r)
+
+        self.layout = layout(0)
         small = self.layout.arena_bytes < (512 << 20)
         # batches that fit the 256 MiB Infinity Cache are rotated so each step reads cold bytes
         nrot = max(1, -(-(768 << 20) // max(self.layout.arena_bytes, 1))) if small else 1
-        self.batches = [DeviceBatch(self.layout if r == 0 else make_layout(
-            config, data_seed=DATA_SEED + 0x1000 * rank + r), self.device) for r in range(nrot)]
+        self.batches = [DeviceBatch(self.layout if r == 0 else layout(r), self.device) for r in range(nrot)]
         self.shape = shape
         self.gather = gather_dist
         self.k = 0
@@ -273,11 +290,13 @@ def main(argv=None):
     args = parse_args(argv)
     dist = Dist()
     shape = tuple(int(x) for x in args.shape.split(",")) if args.shape else None
+    strong = args.scaling == "strong" or (args.scaling == "auto" and args.config == "c5_imix")
     engine = GpuEngine(args.config, dist.rank, dist.local_rank, shape=shape,
-                       gather_dist=dist if args.gather else None, steps=args.steps)
+                       gather_dist=dist if args.gather else None, steps=args.steps, world=dist.world, strong=strong)
     r = timed_loop(engine, dist, args.steps, args.warmup)
     elapsed = r["elapsed_s"]
-    total_bytes = engine.payload_bytes * dist.world * args.steps
+    # all ranks' payload (strong: the shards add up to the config's one batch)
+    total_bytes = int(dist.sum(engine.payload_bytes)) * args.steps
     value = total_bytes / elapsed / 2 ** 30
     kernel_ms = r["kernel_ms"]
     algo_bytes = engine.payload_bytes + 2 * engine.n
@@ -292,7 +311,7 @@ def main(argv=None):
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic: splitmix64 packet bytes (seed 0x5EEDC0DE + per-rank offset), per-packet u16 seeds",
@@ -301,6 +320,7 @@ def main(argv=None):
                         "16 B-aligned arena in HBM, per-packet seed, complemented result (tcp.rs:970 form)",
             "packets_per_gpu": engine.n,
             "payload_bytes_per_gpu": engine.payload_bytes,
+            "batch": "one batch sharded by packet index across ranks" if strong else "a full batch per rank",
             "parallelism": f"packet shards x{dist.world}, no data-path collective"
                            + (" + RCCL all_gather of results" if args.gather else ""),
             "kernel_shape": list(shape) if shape else "auto",

@@ -169,9 +169,11 @@ int rns_rx_verify_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64
  * kernel (one lane stores each result), 1 = rounds kernel (a wave owns 64
  * consecutive packets, one coalesced result store); bit 1: nontemporal packet
  * loads; bit 2: mixed kernel (rounds kernel that sorts each wave's 64 packets
- * into size classes, each with its own shape; G and U are ignored).  lanes_per_packet in
- * {4,8,16,32,64}; unroll (16-byte chunks in flight per lane per pass) in
- * {1,2,4,8}; max_blocks = grid cap (0 = no grid-stride loop). */
+ * into size classes, each with its own shape; G and U are ignored); bit 3 (with
+ * bit 0 only): rounds kernel with every round of a batch in flight (G <= 8, U <= 2).
+ * lanes_per_packet in {4,8,16,32,64} (2 too for the rounds kernel); unroll (16-byte
+ * chunks in flight per lane per pass) in {1,2,4,8}; max_blocks = grid cap (0 = no
+ * grid-stride loop). */
 int rns_csum_batch_dev_cfg(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off,
                            const uint32_t *d_len, const uint16_t *d_seed, uint16_t *d_out, uint32_t n,
                            uint32_t flags, uint32_t variant, uint32_t lanes_per_packet, uint32_t unroll,

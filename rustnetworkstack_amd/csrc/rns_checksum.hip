@@ -488,10 +488,14 @@ __device__ __forceinline__ uint16_t finalize(uint32_t mine, uint64_t d_start, ui
     return finalize_bits(mine, d_start & 1, d_len > kNoWrapBytes, d_seed, d_ok, flags);
 }
 
-template <int G, int U, bool STRIDED, bool NT, bool BUF>
+// D = rounds in flight: 1 = the next round's first pass is issued before the current
+// round is consumed; D = G (small G only) = all rounds of the batch are issued up
+// front, so a batch of tiny packets costs one memory latency instead of G.
+template <int G, int U, bool STRIDED, bool NT, bool BUF, int D = 1>
 __global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
 {
     static_assert(G >= 2 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two in [2,64]");
+    static_assert(D == 1 || (D == G && G <= 8), "deep prefetch: every round of a small-G batch");
     constexpr uint32_t P = 64 / G;  // packets per round
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t sub = lane & (G - 1);
@@ -525,10 +529,26 @@ __global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
         }
 
         uint32_t mine = 0;  // this lane's packet: LE sum (<= 128 KiB) or BE sum (longer)
+        if constexpr (D > 1) {
+            Pkt k[D];
+            uint4 v[D][U];
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+                k[r] = fetch_pkt<G>(d_start, d_len, r * P + grp);
+                issue_pass<G, U, NT, BUF>(a, rsrc, k[r], sub, v[r]);
+            }
+#pragma unroll
+            for (int r = 0; r < D; ++r) {  // consumed oldest first: each wait leaves the later rounds in flight
+                const uint32_t words = group_allreduce<G>(packet_partial<G, U, NT, BUF>(a, rsrc, k[r], sub, v[r]));
+                const uint32_t t = bcast_from<G>(words, (lane % P) * G);
+                mine = (lane / P == static_cast<uint32_t>(r)) ? t : mine;
+            }
+        }
         Pkt cur = fetch_pkt<G>(d_start, d_len, grp);
         uint4 v[U];
-        issue_pass<G, U, NT, BUF>(a, rsrc, cur, sub, v);
-        for (uint32_t r = 0; r < G; ++r) {
+        if constexpr (D == 1)
+            issue_pass<G, U, NT, BUF>(a, rsrc, cur, sub, v);
+        for (uint32_t r = 0; r < (D == 1 ? G : 0); ++r) {
             // Prefetch the next round's first pass.  Unconditional on purpose: on the
             // last round it loads an empty packet (no memory traffic on the buffer
             // path), so every path through the loop has the same loads outstanding
@@ -1136,7 +1156,8 @@ __global__ __launch_bounds__(kBlock) void splitmix64_fill_kernel(uint8_t *buf, u
 
 inline int hip_status(hipError_t e) { return e == hipSuccess ? RNS_OK : RNS_E_HIP_BASE - static_cast<int>(e); }
 
-// Kernel variants: bit 0 = rounds kernel (1) / group kernel (0); bit 1 = nontemporal loads.
+// Kernel variants: bit 0 = rounds kernel (1) / group kernel (0); bit 1 = nontemporal loads;
+// bit 2 = mixed kernel; bit 3 = rounds kernel with every round in flight.
 template <int G, int U, bool S>
 int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipStream_t st)
 {
@@ -1173,6 +1194,19 @@ int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipSt
         } else {
             return RNS_E_INVALID;
         }
+    } else if (variant & 8) {  // rounds kernel, every round in flight (tiny packets)
+        if constexpr (G <= 8 && U <= 2) {
+            if (nt && buf)
+                hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, true, G>), grid, block, 0, st, a);
+            else if (nt)
+                hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, false, G>), grid, block, 0, st, a);
+            else if (buf)
+                hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, false, true, G>), grid, block, 0, st, a);
+            else
+                hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, false, false, G>), grid, block, 0, st, a);
+        } else {
+            return RNS_E_INVALID;
+        }
     } else {
         if (nt && buf)
             hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, true>), grid, block, 0, st, a);
@@ -1189,7 +1223,7 @@ int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipSt
 template <bool S>
 int dispatch(const CsumArgs &a, uint32_t variant, uint32_t G, uint32_t U, uint32_t max_blocks, hipStream_t st)
 {
-    if (variant > 7)
+    if (variant > 15 || ((variant & 8) && (variant & 5) != 1))  // bit 3 (deep prefetch): rounds kernel only
         return RNS_E_INVALID;
     if (variant & 4)  // the mixed kernel picks its own per-class shapes
         return launch_shape<64, 4, S>(a, variant, max_blocks, st);
@@ -1774,8 +1808,8 @@ const char *rns_csum_shape_name(uint32_t len_hint)
     if (sh.variant & 4)
         std::snprintf(buf, sizeof(buf), "%s (size classes G/U 4/1, 4/4, 16/4, 32/4, 64/4)", names[sh.variant & 7]);
     else
-        std::snprintf(buf, sizeof(buf), "%s<G=%u,U=%u>%s", names[sh.variant & 7], sh.G, sh.U,
-                      sh.max_blocks ? " grid-capped" : "");
+        std::snprintf(buf, sizeof(buf), "%s<G=%u,U=%u>%s%s", names[sh.variant & 7], sh.G, sh.U,
+                      (sh.variant & 8) ? " all rounds in flight" : "", sh.max_blocks ? " grid-capped" : "");
     return buf;
 }
 

@@ -46,7 +46,8 @@ r = bench.timed_loop(eng, d, steps=3, warmup=1)
 import torch, torch.distributed as dist
 outs = [torch.zeros(0) for _ in range(d.world)]
 obj = [None] * d.world
-dist.all_gather_object(obj, (d.rank, eng.n, eng.out.tolist(), r["local_elapsed_s"], r["elapsed_s"]))
+dist.all_gather_object(obj, (d.rank, eng.n, eng.out.tolist(), r["local_elapsed_s"], r["elapsed_s"],
+                             d.sum(eng.payload_bytes)))
 if d.rank == 0:
     print(json.dumps(obj))
 d.close()
@@ -81,7 +82,9 @@ def test_two_rank_gloo_harness(tmp_path, oracle):
     from rustnetworkstack_amd.workloads import make_layout
     total = sum(x[1] for x in ranks)
     assert total == 40000
-    for rank, n, out, _, _ in ranks:
+    # strong scaling's aggregate: the shards' payload adds up to the one batch's, on every rank
+    assert {x[5] for x in ranks} == {make_layout("c5_imix", n=40000).payload_bytes}
+    for rank, n, out, _, _, _ in ranks:
         lay = make_layout("c5_imix", n=40000, shard=(rank, 2))
         arena = splitmix64_bytes(lay.data_seed, lay.arena_bytes)
         assert np.array_equal(np.array(out, dtype=np.uint16),

@@ -22,6 +22,7 @@ DEV = "cuda:0"
 SHAPES = [(var, g, u) for var in (0, 1) for g in (4, 8, 16, 32, 64) for u in (1, 2, 4, 8)]
 SHAPES += [(var, 64, 4) for var in (2, 3, 4, 6)]
 SHAPES += [(var, 2, u) for var in (1, 3) for u in (1, 2, 4)]  # 2-lane groups: rounds kernel only
+SHAPES += [(var, g, u) for var in (9, 11) for g in (2, 4, 8) for u in (1, 2)]  # every round in flight
 
 
 def host_u16(t: torch.Tensor) -> np.ndarray:
@@ -256,5 +257,6 @@ def test_packets_ending_at_unpadded_arena_end(oracle, total):
     sd = np.arange(len(lens), dtype=np.uint16) * np.uint16(4099)
     expect = oracle.batch(arena_np, off, lens, sd)
     d = dev_desc(off, lens, sd)
-    for shape in [None] + [(v, g, u, 0) for v in range(8) for g, u in ((4, 1), (16, 4), (64, 2))]:
+    for shape in [None] + [(v, g, u, 0) for v in range(8) for g, u in ((4, 1), (16, 4), (64, 2))] + \
+            [(9, 4, 1, 0), (11, 2, 2, 0), (11, 8, 1, 3)]:
         assert np.array_equal(host_u16(csum_batch(arena, *d, shape=shape)), expect), shape
