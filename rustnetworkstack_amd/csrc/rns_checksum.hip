@@ -1104,194 +1104,6 @@ __global__ __launch_bounds__(kBlock, (BUF && !FILL && !RX) ? RNS_MIXED_OCC : 3) 
 }
 
 // ---------------------------------------------------------------------------
-// v4: "flat" kernel — a wavefront owns 64 consecutive packets and streams the
-// CONCATENATION of their 16-byte chunks, 64 chunks (1 KB) per round whatever the
-// packet sizes: lane l of round r takes chunk j = 64r + l of the list.  Every round
-// is a full coalesced 1 KB (the mixed kernel's rounds shrink with the packets), and
-// D rounds are in flight.  Per round, in LDS:
-//   * which lanes start a packet: each packet whose first chunk E_i falls in the
-//     round's window marks slot E_i - 64r (zero, scatter, read: no conflicts);
-//     ballot -> M, and a lane's packet is the count of starts before it (mbcnt);
-//   * that packet's record (chunk-0 offset, E, s | e-1 | nch) -> the chunk address;
-//   * after the data arrives: an inclusive DPP scan of the lanes' chunk sums, and the
-//     last lane of each packet's run adds (its prefix - the prefix before the run) to
-//     the packet's LDS accumulator (one ds_add per run, distinct addresses).
-// Batches holding a packet longer than 128 KiB (never an IP packet) take a plain
-// whole-wave-per-packet pass with the exact big-endian sums instead.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane)
-{
-    v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xF, 0xF, false));  // row_shr:1
-    v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xF, 0xF, false));  // row_shr:2
-    v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xF, 0xF, false));  // row_shr:4
-    v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xF, 0xF, false));  // row_shr:8
-    const uint32_t r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31),
-                   r2 = __builtin_amdgcn_readlane(v, 47);
-    v += (lane >= 16 ? r0 : 0u) + (lane >= 32 ? r1 : 0u) + (lane >= 48 ? r2 : 0u);
-    return v;
-}
-
-struct FlatRound {
-    uint4 x;        // the chunk
-    uint32_t lohi;  // keep bytes [lo, hi): lo | hi << 8
-    uint32_t q;     // compact index of the chunk's packet
-    uint64_t m;     // lanes that start a packet this round
-};
-
-template <bool NT, bool BUF>
-__device__ __forceinline__ FlatRound flat_issue(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint32_t *flag,
-                                                const uint4 *rec, uint32_t E, bool ne, uint32_t r, uint32_t T,
-                                                uint32_t lane, uint32_t &C)
-{
-    const uint32_t W = r * 64;
-    flag[lane] = 0;
-    wave_lds_fence();
-    const uint32_t t = E - W;
-    if (ne && t < 64u)
-        flag[t] = 1;
-    wave_lds_fence();
-    const uint32_t h = flag[lane];
-    FlatRound fr;
-    fr.m = __ballot(h != 0);
-    const uint32_t below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(fr.m >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(fr.m), 0u));
-    const uint32_t q = C + below + h - 1u;  // lanes before the window's first start: the packet from before
-    C += static_cast<uint32_t>(__popcll(fr.m));
-    const uint32_t j = W + lane;
-    const bool valid = j < T;
-    fr.q = q;  // past the list's end: the last packet (its run's end lane adds the run's sum)
-    const uint4 rc = rec[valid ? q : 0u];   // {chunk-0 offset lo, hi, E, s | (e-1) << 4 | nch << 8}
-    const uint32_t c = j - rc.z;
-    const uint32_t nch = rc.w >> 8, s = rc.w & 15u, e = ((rc.w >> 4) & 15u) + 1u;
-    fr.lohi = (c == 0 ? s : 0u) | ((c + 1 == nch ? e : 16u) << 8);
-    const uint64_t o = ((static_cast<uint64_t>(rc.y) << 32) | rc.x) + (static_cast<uint64_t>(c) << 4);
-    if constexpr (BUF) {
-        const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rsrc, valid ? static_cast<uint32_t>(o) : kOobOffset, 0,
-                                                              NT ? 2 : 0);
-        fr.x = make_uint4(y.x, y.y, y.z, y.w);
-    } else {
-        const uint4 y = load_chunk<NT>(a.arena + (valid ? o : 0));
-        fr.x = valid ? y : make_uint4(0, 0, 0, 0);
-    }
-    return fr;
-}
-
-__device__ __forceinline__ void flat_consume(FlatRound &fr, uint32_t *acc, uint32_t lane)
-{
-    const int lo = static_cast<int>(fr.lohi & 0xff), hi = static_cast<int>(fr.lohi >> 8);
-    if (lo != 0 || hi != 16) {
-        fr.x.x = keep_bytes(fr.x.x, lo, hi, 0);
-        fr.x.y = keep_bytes(fr.x.y, lo, hi, 4);
-        fr.x.z = keep_bytes(fr.x.z, lo, hi, 8);
-        fr.x.w = keep_bytes(fr.x.w, lo, hi, 12);
-    }
-    uint32_t v = __builtin_amdgcn_sad_u16(fr.x.x, 0, 0u);
-    v = __builtin_amdgcn_sad_u16(fr.x.y, 0, v);
-    v = __builtin_amdgcn_sad_u16(fr.x.z, 0, v);
-    v = __builtin_amdgcn_sad_u16(fr.x.w, 0, v);
-    const uint32_t S = wave_incl_scan(v, lane);
-    // first lane of this lane's run of equal packets: the highest start at or below it
-    const uint64_t upto = fr.m & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
-    const uint32_t a0 = upto ? 63u - static_cast<uint32_t>(__builtin_clzll(upto)) : 0u;
-    const uint32_t before = static_cast<uint32_t>(__shfl(static_cast<int>(S), static_cast<int>(a0 ? a0 - 1 : 0), 64));
-    const bool end = lane == 63 || ((fr.m >> (lane + 1)) & 1ull);
-    if (end)
-        atomicAdd(&acc[fr.q], S - (a0 ? before : 0u));
-}
-
-template <bool STRIDED, bool NT, bool BUF, int D>
-__global__ __launch_bounds__(kBlock) void csum_flat_kernel(const CsumArgs a)
-{
-    static_assert(D >= 1 && D <= 8, "rounds in flight");
-    __shared__ uint32_t lds_flag[kBlock / 64][64];
-    __shared__ uint4 lds_rec[kBlock / 64][64];
-    __shared__ uint32_t lds_acc[kBlock / 64][64];
-    const uint32_t wv = threadIdx.x >> 6;
-    uint32_t *const flag = lds_flag[wv];
-    uint4 *const rec = lds_rec[wv];
-    uint32_t *const acc = lds_acc[wv];
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
-
-    for (uint64_t base = static_cast<uint64_t>(wave) * 64; base < a.n; base += static_cast<uint64_t>(nwaves) * 64) {
-        const uint64_t p = base + lane;
-        const bool live = p < a.n;
-        const Desc<BUF> cd = load_desc<STRIDED, false, BUF>(a, p);
-        uint64_t d_start = cd.off + a.base_adjust;
-        uint32_t d_len = cd.len;
-        const uint32_t d_seed = (a.seed && live) ? a.seed[p] : 0u;
-        const bool d_ok = d_start <= a.arena_bytes && d_len <= a.arena_bytes - d_start;
-        if (!d_ok || d_len == 0) {
-            d_len = 0;
-            d_start = 0;
-        }
-        const bool odd = d_start & 1;
-        uint32_t mine = 0;
-        bool big_batch = __ballot(d_len > kNoWrapBytes) != 0;  // wave-uniform
-        if (!big_batch) {
-            const uint32_t s = static_cast<uint32_t>(d_start & 15);
-            const uint32_t nch = d_len ? (s + d_len + 15) >> 4 : 0u;  // <= 8193
-            const uint32_t e = d_len ? s + d_len - 16 * (nch - 1) : 1u;
-            const uint32_t incl = wave_incl_scan(nch, lane);
-            const uint32_t E = incl - nch, T = __builtin_amdgcn_readlane(incl, 63);
-            const bool ne = nch != 0;
-            const uint64_t nem = __ballot(ne);
-            const uint32_t qi = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(nem >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(nem), 0u));
-            const uint64_t first = d_start - s;
-            if (ne)
-                rec[qi] = make_uint4(static_cast<uint32_t>(first), static_cast<uint32_t>(first >> 32), E,
-                                     s | ((e - 1) << 4) | (nch << 8));
-            acc[lane] = 0;
-            wave_lds_fence();  // records and zeroed accumulators are read / added to by other lanes
-            const uint32_t R = (T + 63) / 64;
-            uint32_t C = 0;
-            FlatRound fr[D];
-#pragma unroll
-            for (int k = 0; k < D; ++k)
-                fr[k] = flat_issue<NT, BUF>(a, rsrc, flag, rec, E, ne, k, T, lane, C);
-            for (uint32_t r0 = 0; r0 < R; r0 += D) {
-#pragma unroll
-                for (int k = 0; k < D; ++k) {
-                    flat_consume(fr[k], acc, lane);  // rounds past R hold zeros: harmless
-                    fr[k] = flat_issue<NT, BUF>(a, rsrc, flag, rec, E, ne, r0 + k + D, T, lane, C);
-                }
-            }
-            wave_lds_fence();
-            mine = ne ? acc[qi] : 0u;
-        } else {
-            // rare: some packet > 128 KiB; every packet of the batch by the whole wave, exact BE sums
-            for (uint32_t i = 0; i < 64; ++i) {
-                const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(d_start), i);
-                const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(d_start >> 32), i);
-                const Pkt k = make_pkt((static_cast<uint64_t>(hi) << 32) | lo, __builtin_amdgcn_readlane(d_len, i));
-                const uint32_t w_hi = (k.start & 1) ? 0x01000100u : 0x00010001u;
-                uint32_t hs = 0, ls = 0;
-                for (uint32_t c0 = lane; c0 < k.nch; c0 += 64 * 4) {
-                    uint4 v[4];
-                    issue_pass<64, 4, NT, BUF>(a, rsrc, k, c0, v);
-                    mask_edges<64, 4>(k, c0, v);
-                    sum_be<4>(v, w_hi, hs, ls);
-                }
-                const uint32_t tot = group_allreduce<64>((hs << 8) + ls);
-                mine = lane == i ? tot : mine;
-            }
-        }
-        const uint16_t res = finalize_bits(mine, odd, big_batch, d_seed, d_ok, a.flags);
-        if (live)
-            a.out[p] = res;  // 64 consecutive u16: one 128-byte store
-        if (a.bad) {
-            const uint64_t rejected = __ballot(live && !d_ok);
-            if (rejected && lane == 0)
-                atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Fragment chains (util.rs:112-119 compute_buffer_ones_comp over NetBuffer
 // fragments, buf.rs:466-487).  Pass 1 is the packet kernel run over FRAGMENTS
 // with seed 0: frag_sums[f] = compute_ones_comp(0, fragment f), pairing bytes from
@@ -1359,7 +1171,7 @@ template <int G, int U, bool S>
 int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipStream_t st)
 {
     uint64_t blocks;
-    if ((variant & 21) == 0) {
+    if ((variant & 5) == 0) {
         constexpr uint32_t kGroups = kBlock / G;
         blocks = (static_cast<uint64_t>(a.n) + kGroups - 1) / kGroups;
     } else {
@@ -1373,20 +1185,7 @@ int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipSt
     const dim3 grid(static_cast<uint32_t>(blocks)), block(kBlock);
     const bool nt = (variant & 2) != 0;
     const bool buf = buf_records(a) < kOobOffset;  // buffer loads need a 32-bit offset range
-    if (variant & 16) {  // flat kernel; U = rounds in flight
-        if constexpr (U == 2 || U == 4 || U == 8) {
-            if (nt && buf)
-                hipLaunchKernelGGL((csum_flat_kernel<S, true, true, U>), grid, block, 0, st, a);
-            else if (nt)
-                hipLaunchKernelGGL((csum_flat_kernel<S, true, false, U>), grid, block, 0, st, a);
-            else if (buf)
-                hipLaunchKernelGGL((csum_flat_kernel<S, false, true, U>), grid, block, 0, st, a);
-            else
-                hipLaunchKernelGGL((csum_flat_kernel<S, false, false, U>), grid, block, 0, st, a);
-        } else {
-            return RNS_E_INVALID;
-        }
-    } else if (variant & 4) {
+    if (variant & 4) {
         if (nt && buf)
             hipLaunchKernelGGL((csum_mixed_kernel<S, true, true, false>), grid, block, 0, st, a);
         else if (nt)
@@ -1433,16 +1232,8 @@ int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipSt
 template <bool S>
 int dispatch(const CsumArgs &a, uint32_t variant, uint32_t G, uint32_t U, uint32_t max_blocks, hipStream_t st)
 {
-    if (variant > 31 || ((variant & 8) && (variant & 21) != 1))  // bit 3 (deep prefetch): rounds kernel only
+    if (variant > 15 || ((variant & 8) && (variant & 5) != 1))  // bit 3 (deep prefetch): rounds kernel only
         return RNS_E_INVALID;
-    if ((variant & 16) && (variant & 13))  // bit 4 (flat kernel): with bit 1 (nontemporal) only
-        return RNS_E_INVALID;
-    if (variant & 16) {  // flat kernel: U = rounds in flight
-        if (U == 2) return launch_shape<64, 2, S>(a, variant, max_blocks, st);
-        if (U == 4) return launch_shape<64, 4, S>(a, variant, max_blocks, st);
-        if (U == 8) return launch_shape<64, 8, S>(a, variant, max_blocks, st);
-        return RNS_E_INVALID;
-    }
     if (variant & 4)  // the mixed kernel picks its own per-class shapes
         return launch_shape<64, 4, S>(a, variant, max_blocks, st);
 #define RNS_SHAPE(g, u) \
