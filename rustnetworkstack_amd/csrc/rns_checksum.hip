@@ -39,7 +39,10 @@
 
 namespace {
 
-constexpr int kBlock = 256;
+#ifndef RNS_BLOCK
+#define RNS_BLOCK 256
+#endif
+constexpr int kBlock = RNS_BLOCK;  // threads per workgroup (A/B knob: 64..1024)
 
 struct CsumArgs {
     const uint8_t *arena;      // 16-byte aligned base
@@ -904,6 +907,13 @@ __device__ __forceinline__ Desc<BUF> load_desc(const CsumArgs &a, uint64_t p)
     return d;
 }
 
+// Workgroup size of the mixed kernel: receive verify and transmit fill hold an LDS
+// stash per wave, and LDS is freed per WORKGROUP, so one-wave workgroups let a CU
+// refill as soon as any wave finishes (IMIX verify 590 -> 559 us); the plain batch
+// has no LDS and keeps 4-wave workgroups.
+template <bool STASH>
+constexpr int kMixedBlock = STASH ? 64 : kBlock;
+
 // FILL (transmit in-place fill, tcp.rs:957-973 / udp.rs:158-171 / icmp.rs:87-112 /
 // ip.rs:158-159): the checksum is that of the packet with its 2-byte field zeroed
 // (alloc_header zero-fills it, buf.rs:286-288).  The data pass sums the whole packet;
@@ -915,18 +925,19 @@ template <bool STRIDED, bool NT, bool BUF, bool FILL, bool RX = false>
 #ifndef RNS_MIXED_OCC
 #define RNS_MIXED_OCC 4
 #endif
-__global__ __launch_bounds__(kBlock, (BUF && !FILL && !RX) ? RNS_MIXED_OCC : 3) void csum_mixed_kernel(const CsumArgs a)
+__global__ __launch_bounds__(kMixedBlock<FILL || RX>, (BUF && !FILL && !RX) ? RNS_MIXED_OCC : 3) void csum_mixed_kernel(const CsumArgs a)
 {
     static_assert(!(FILL && RX) && !(STRIDED && RX), "one mode at a time");
     constexpr int kMode = RX ? kStashHead : FILL ? kStashField : kStashNone;
     constexpr int kNS = kStashChunks<kMode>;
     constexpr uint32_t kPer = 64;  // packets per wave batch
     // per wave: kNS chunks for each of its 64 packets, indexed by sorted position
-    __shared__ uint4 stash_lds[kNS ? (kBlock / 64) * kPer * kNS : 1];
+    constexpr int BLK = kMixedBlock<FILL || RX>;
+    __shared__ uint4 stash_lds[kNS ? (BLK / 64) * kPer * kNS : 1];
     uint4 *const st = stash_lds + (threadIdx.x >> 6) * (kPer * kNS);
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
+    const uint32_t wave = (blockIdx.x * BLK + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * BLK) >> 6;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
 
@@ -1466,8 +1477,9 @@ int rns_csum_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_
     a.flags = flags;
     a.field = d_field;
     a.field_off = field_off;
-    const uint64_t blocks = ((static_cast<uint64_t>(n) + 63) / 64 + kBlock / 64 - 1) / (kBlock / 64);
-    const dim3 grid(static_cast<uint32_t>(blocks)), block(kBlock);
+    constexpr int BLK = kMixedBlock<true>;
+    const uint64_t blocks = ((static_cast<uint64_t>(n) + 63) / 64 + BLK / 64 - 1) / (BLK / 64);
+    const dim3 grid(static_cast<uint32_t>(blocks)), block(BLK);
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (buf_records(a) < kOobOffset)
         hipLaunchKernelGGL((csum_mixed_kernel<false, false, true, true>), grid, block, 0, st, a);
@@ -1505,7 +1517,8 @@ int rns_rx_verify_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64
     a.local4_sum = be_sum(local_ipv4, 4);
     a.local6_sum = be_sum(local_ipv6, 16);
     const uint64_t waves = (static_cast<uint64_t>(n) + 63) / 64;  // 64 datagrams per wave
-    const dim3 grid(static_cast<uint32_t>((waves + kBlock / 64 - 1) / (kBlock / 64))), block(kBlock);
+    constexpr int BLK = kMixedBlock<true>;
+    const dim3 grid(static_cast<uint32_t>((waves + BLK / 64 - 1) / (BLK / 64))), block(BLK);
     hipStream_t st = static_cast<hipStream_t>(stream);
 #ifdef RNS_RX_PLAIN
     constexpr bool kNT = false;
