@@ -751,7 +751,7 @@ struct RxParse {
 
 // The first 24 bytes of a datagram (every field rx_parse reads) as six dwords in
 // datagram byte order, from the stashed chunks 0..2 (s = start & 15).
-__device__ __forceinline__ void head_from_stash(const uint4 (&ch)[5], uint32_t s, uint32_t (&h)[6])
+__device__ __forceinline__ void head_from_stash(const uint4 (&ch)[3], uint32_t s, uint32_t (&h)[6])
 {
     const uint32_t w[12] = {ch[0].x, ch[0].y, ch[0].z, ch[0].w, ch[1].x, ch[1].y,
                             ch[1].z, ch[1].w, ch[2].x, ch[2].y, ch[2].z, ch[2].w};
@@ -1019,11 +1019,12 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX>, (BUF && !FILL && !RX) ? RN
             // mine = the whole datagram's word sum T.  Header H from the stash (seed 0,
             // <= 60 bytes); L4 = T - H, seeded with the pseudo-header sum.  Both parts
             // start at the datagram's parity (the header length is even).
-            uint4 ch[kNS];
+            uint4 ch[3];
             wave_lds_fence();  // the stash was written by other lanes of this wave
+            const uint4 *mine_st = st + pos * kNS;
 #pragma unroll
-            for (int i = 0; i < kNS; ++i)
-                ch[i] = st[pos * kNS + i];
+            for (int i = 0; i < 3; ++i)
+                ch[i] = mine_st[i];
             const uint32_t s = static_cast<uint32_t>(d_start & 15);
             uint32_t head[6];
             head_from_stash(ch, s, head);
@@ -1032,10 +1033,20 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX>, (BUF && !FILL && !RX) ? RN
             uint32_t hdr_res = 0, l4_res = 0;
             if (!(rp.meta & kMetaMalformed)) {
                 const int hlo = static_cast<int>(s), hhi = hlo + static_cast<int>(rp.hdr);  // <= 15 + 60
-                const uint32_t H = stash_sum_le(ch, hlo, hhi);
+                uint32_t H = stash_sum_le(ch, hlo, hhi);
+                uint4 tail[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+                if (hhi > 48) {  // IPv6 past offset 8, IPv4 with options: header bytes in chunks 3-4
+                    tail[0] = mine_st[3];
+                    tail[1] = mine_st[4];
+                    H += stash_sum_le(tail, hlo - 48, hhi - 48);
+                }
                 hdr_res = finalize_bits(H, odd, false, 0u, true, RNS_FLAG_COMPLEMENT);
                 if (rp.meta & kMetaL4Checked) {
-                    const uint32_t l4 = big ? mine - stash_sum_be(ch, hlo, hhi, odd) : mine - H;
+                    uint32_t l4 = mine - H;
+                    if (big) {  // > 128 KiB (rare): the exact big-endian sums, mod 2^32
+                        const uint4 all[5] = {ch[0], ch[1], ch[2], tail[0], tail[1]};
+                        l4 = mine - stash_sum_be(all, hlo, hhi, odd);
+                    }
                     l4_res = finalize_bits(l4, odd, big, rp.ph, true, RNS_FLAG_COMPLEMENT);
                 }
             }
