@@ -606,15 +606,21 @@ struct ClassRun {
 };
 
 // Size classes (16-byte chunks a packet spans) and the shape each class runs with.
-constexpr uint32_t kNumClasses = 5;
-constexpr uint32_t kClassMax[kNumClasses - 1] = {4, 16, 64, 128};  // above the last: jumbo
-// (A/B builds override these: -DRNS_CLASS_LOG2G=1,2,4,5,6 -DRNS_CLASS_U=2,4,4,4,4)
+// (A/B builds override these: -DRNS_CLASS_MAX=4,16,32,64,128 -DRNS_CLASS_LOG2G=2,2,3,4,5,6
+//  -DRNS_CLASS_U=1,4,4,4,4,4 — the class count follows RNS_CLASS_MAX, at most 6)
+#ifndef RNS_CLASS_MAX
+#define RNS_CLASS_MAX 4, 16, 64, 128
+#endif
 #ifndef RNS_CLASS_LOG2G
 #define RNS_CLASS_LOG2G 2, 2, 4, 5, 6
 #endif
 #ifndef RNS_CLASS_U
 #define RNS_CLASS_U 1, 4, 4, 4, 4
 #endif
+constexpr uint32_t kClassMaxList[] = {RNS_CLASS_MAX};                 // above the last: jumbo
+constexpr uint32_t kNumClasses = sizeof(kClassMaxList) / sizeof(kClassMaxList[0]) + 1;
+static_assert(kNumClasses <= 6, "at most 6 size classes");
+constexpr const uint32_t (&kClassMax)[kNumClasses - 1] = kClassMaxList;
 constexpr uint32_t kClassLog2G[kNumClasses] = {RNS_CLASS_LOG2G};   // lanes per packet 4, 4, 16, 32, 64
 constexpr uint32_t kClassU[kNumClasses] = {RNS_CLASS_U};           // chunks in flight per lane
 constexpr int kUMax = 4;
@@ -1013,6 +1019,8 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX>, (BUF && !FILL && !RX) ? RN
         RNS_RUN_CLASS(2);
         RNS_RUN_CLASS(3);
         RNS_RUN_CLASS(4);
+        if constexpr (kNumClasses > 5)
+            RNS_RUN_CLASS(5 % kNumClasses);
 #undef RNS_RUN_CLASS
 
         if constexpr (RX) {
