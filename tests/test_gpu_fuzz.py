@@ -1,0 +1,168 @@
+"""Randomised parity and concurrency tests of the GPU entry points against the oracle.
+
+* random descriptor sets (lengths 0..20000, any alignment, overlapping packets,
+  descriptors outside the arena) through every kernel family and the default shape
+  picked for several length hints;
+* arbitrary bytes as received datagrams (rx_verify must agree with the reference's
+  receive path on garbage too, ip.rs:38-128);
+* concurrent callers: host batches from several threads (one staging context each,
+  the threading model of SURVEY §8b) and device batches on several streams.
+"""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from rustnetworkstack_amd.batch import HostBatcher, csum_batch, rx_verify
+from test_rx_oracle import L4, L6
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+ARENA = 8 << 20
+
+
+def dev(a, view):
+    return torch.from_numpy(np.ascontiguousarray(a).view(view)).to(DEV)
+
+
+def host_u16(t):
+    torch.cuda.synchronize()
+    return t.view(torch.int16).cpu().numpy().view(np.uint16)
+
+
+def random_batch(seed, n, arena_bytes=ARENA, invalid_frac=0.02):
+    w = O.splitmix64_words(seed, 4 * n).reshape(n, 4)
+    kind = w[:, 0] % np.uint64(10)
+    ln = np.empty(n, dtype=np.uint64)
+    ln[kind < 3] = w[kind < 3, 1] % np.uint64(64) + np.uint64(1)
+    mid = (kind >= 3) & (kind < 6)
+    ln[mid] = w[mid, 1] % np.uint64(1936) + np.uint64(65)
+    big = (kind >= 6) & (kind < 8)
+    ln[big] = w[big, 1] % np.uint64(18000) + np.uint64(2001)
+    ln[kind == 8] = 0
+    imix = kind == 9
+    ln[imix] = np.array([40, 576, 1500], dtype=np.uint64)[(w[imix, 1] % np.uint64(3)).astype(np.int64)]
+    off = w[:, 2] % (np.uint64(arena_bytes) - ln + np.uint64(1))          # inside, overlapping freely
+    bad = (w[:, 3] % np.uint64(10000)) < np.uint64(invalid_frac * 10000)
+    off[bad] = np.uint64(arena_bytes) - ln[bad] + np.uint64(1) + (w[bad, 3] % np.uint64(5000))   # past the end
+    sd = (w[:, 3] >> np.uint64(20)).astype(np.uint16)
+    return off, ln.astype(np.uint32), sd, bad
+
+
+def expected(oracle, arena_np, off, ln, sd, bad, complement):
+    ok = ~bad & (ln > 0)
+    exp = np.zeros(off.shape[0], dtype=np.uint16)
+    exp[ok] = oracle.batch(arena_np, off[ok], ln[ok], sd[ok], complement=complement)
+    empty = ~bad & (ln == 0)  # API-defined: the seed (the reference panics, util.rs:92)
+    exp[empty] = (sd[empty] ^ np.uint16(0xFFFF)) if complement else sd[empty]
+    return exp
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_descriptors_every_kernel(oracle, seed):
+    arena_np = O.splitmix64_bytes(0xF0 + seed, ARENA)
+    arena = torch.from_numpy(arena_np).to(DEV)
+    off, ln, sd, bad = random_batch(0xAB00 + seed, 30000)
+    complement = bool(seed & 1)
+    exp = expected(oracle, arena_np, off, ln, sd, bad, complement)
+    d = (dev(off, np.int64), dev(ln, np.int32), dev(sd, np.int16))
+    shapes = [None, (4, 0, 0, 0), (6, 0, 0, 0), (6, 0, 0, 41), (3, 4, 1, 2048), (11, 4, 1, 0), (1, 32, 4, 0),
+              (2, 64, 4, 0), (0, 16, 2, 0)]
+    for shape in shapes:
+        for hint in ((40, 340, 1500, 9000) if shape is None else (0,)):
+            cnt = torch.zeros(1, dtype=torch.int32, device=DEV)
+            got = host_u16(csum_batch(arena, *d, complement=complement, shape=shape, len_hint=hint, bad=cnt))
+            mism = np.nonzero(got != exp)[0]
+            assert mism.size == 0, (shape, hint, [(int(i), int(off[i]), int(ln[i]), int(got[i]), int(exp[i]))
+                                                  for i in mism[:5]])
+            assert int(cnt.item()) == int(bad.sum()), (shape, hint)
+
+
+def test_garbage_datagrams_match_reference_receive_path(oracle):
+    n = 6000
+    w = O.splitmix64_words(0x6A4B, 2 * n)
+    pkts = []
+    for i in range(n):
+        L = int(w[2 * i] % np.uint64(3000))
+        p = bytearray(O.splitmix64_bytes(int(w[2 * i + 1]), L).tobytes())
+        if L and i % 3 == 0:
+            p[0] = 0x40 | (p[0] & 0x0F)            # version 4, random IHL
+        elif L and i % 3 == 1:
+            p[0] = 0x60 | (p[0] & 0x0F)            # version 6
+        pkts.append(bytes(p))
+    offs, pos = [], 0
+    for i, p in enumerate(pkts):
+        pos += int(w[2 * i] >> np.uint64(40)) % 16
+        offs.append(pos)
+        pos += len(p)
+    arena_np = np.zeros(pos + 64, dtype=np.uint8)
+    for o, p in zip(offs, pkts):
+        arena_np[o:o + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    off = np.array(offs, dtype=np.uint64)
+    ln = np.array([len(p) for p in pkts], dtype=np.uint32)
+    want = [O.rx_verify_ref(p, L4, L6, ones_comp=oracle.compute_ones_comp) for p in pkts]
+    l4 = torch.empty(n, dtype=torch.uint16, device=DEV)
+    st = rx_verify(torch.from_numpy(arena_np).to(DEV), dev(off, np.int64), dev(ln, np.int32), L4, L6, l4_sum=l4)
+    got = list(zip(st.cpu().numpy().tolist(), host_u16(l4).tolist()))
+    bad = [(i, len(pkts[i]), got[i], want[i]) for i in range(n) if got[i] != tuple(want[i])]
+    assert not bad, bad[:5]
+
+
+def test_host_batches_from_concurrent_threads(oracle):
+    """One staging context per thread, as the receive, timer and application threads
+    of the stack would hold; the C calls release the GIL."""
+    jobs = []
+    for t in range(4):
+        arena_np = O.splitmix64_bytes(0x7700 + t, 4 << 20)
+        n = 4000 + 1000 * t
+        w = O.splitmix64_words(0x7800 + t, n)
+        ln = (w % np.uint64(1700) + np.uint64(1)).astype(np.uint32)
+        off = np.zeros(n, dtype=np.uint64)
+        np.cumsum((ln[:-1].astype(np.uint64) + np.uint64(3)), out=off[1:])  # ascending, packed, odd gaps
+        keep = off + ln <= arena_np.shape[0]
+        off, ln = off[keep], ln[keep]
+        sd = (w[:off.shape[0]] >> np.uint64(32)).astype(np.uint16)
+        jobs.append((arena_np, off, ln, sd, oracle.batch(arena_np, off, ln, sd, complement=True)))
+    errors, results = [], [None] * len(jobs)
+
+    def work(k):
+        try:
+            hb = HostBatcher(device=0, chunk_bytes=1 << 20, nstreams=2)
+            for _ in range(3):
+                arena_np, off, ln, sd, _ = jobs[k]
+                results[k] = hb.run(arena_np, off, ln, sd, complement=True)
+                if not np.array_equal(results[k], jobs[k][4]):
+                    errors.append(k)
+            hb.close()
+        except Exception as e:  # noqa: BLE001 — reported below
+            errors.append((k, repr(e)))
+
+    threads = [threading.Thread(target=work, args=(k,)) for k in range(len(jobs))]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    assert not errors, errors
+    assert all(r is not None for r in results)
+
+
+def test_device_batches_on_concurrent_streams(oracle):
+    arena_np = O.splitmix64_bytes(0x5151, ARENA)
+    arena = torch.from_numpy(arena_np).to(DEV)
+    streams = [torch.cuda.Stream(device=DEV) for _ in range(3)]
+    cases = []
+    for k in range(len(streams)):
+        off, ln, sd, bad = random_batch(0x5200 + k, 20000, invalid_frac=0.0)
+        cases.append((dev(off, np.int64), dev(ln, np.int32), dev(sd, np.int16),
+                      expected(oracle, arena_np, off, ln, sd, bad, False)))
+    torch.cuda.synchronize()
+    outs = []
+    for rep in range(4):
+        for st, (d_off, d_len, d_sd, _) in zip(streams, cases):
+            with torch.cuda.stream(st):
+                outs.append(csum_batch(arena, d_off, d_len, d_sd, len_hint=(40, 576, 1500)[rep % 3]))
+    torch.cuda.synchronize()
+    for i, out in enumerate(outs):
+        assert np.array_equal(host_u16(out), cases[i % len(streams)][3]), i
