@@ -170,7 +170,9 @@ int rns_rx_verify_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64
  * consecutive packets, one coalesced result store); bit 1: nontemporal packet
  * loads; bit 2: mixed kernel (rounds kernel that sorts each wave's 64 packets
  * into size classes, each with its own shape; G and U are ignored); bit 3 (with
- * bit 0 only): rounds kernel with every round of a batch in flight (G <= 8, U <= 2).
+ * bit 0 only): rounds kernel with every round of a batch in flight (G <= 8, U <= 2);
+ * bits 8-11: at most that many 4-wave workgroups per CU (an occupancy cap, by LDS
+ * reservation; 0 = none).
  * lanes_per_packet in {4,8,16,32,64} (2 too for the rounds kernel); unroll (16-byte
  * chunks in flight per lane per pass) in {1,2,4,8}; max_blocks = grid cap (0 = no
  * grid-stride loop). */

@@ -1215,46 +1215,51 @@ int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipSt
     const dim3 grid(static_cast<uint32_t>(blocks)), block(kBlock);
     const bool nt = (variant & 2) != 0;
     const bool buf = buf_records(a) < kOobOffset;  // buffer loads need a 32-bit offset range
+    // Variant bits 8-11 (tuning): at most that many workgroups per CU, i.e. waves per
+    // SIMD for 4-wave workgroups, by reserving LDS (160 KB per CU on gfx950).
+    const uint32_t cap = (variant >> 8) & 15u;
+    const size_t lds = cap ? ((160u << 10) / cap) - (2u << 10) : 0u;
+    variant &= 0xffu;
     if (variant & 4) {
         if (nt && buf)
-            hipLaunchKernelGGL((csum_mixed_kernel<S, true, true, false>), grid, block, 0, st, a);
+            hipLaunchKernelGGL((csum_mixed_kernel<S, true, true, false>), grid, block, lds, st, a);
         else if (nt)
-            hipLaunchKernelGGL((csum_mixed_kernel<S, true, false, false>), grid, block, 0, st, a);
+            hipLaunchKernelGGL((csum_mixed_kernel<S, true, false, false>), grid, block, lds, st, a);
         else if (buf)
-            hipLaunchKernelGGL((csum_mixed_kernel<S, false, true, false>), grid, block, 0, st, a);
+            hipLaunchKernelGGL((csum_mixed_kernel<S, false, true, false>), grid, block, lds, st, a);
         else
-            hipLaunchKernelGGL((csum_mixed_kernel<S, false, false, false>), grid, block, 0, st, a);
+            hipLaunchKernelGGL((csum_mixed_kernel<S, false, false, false>), grid, block, lds, st, a);
     } else if ((variant & 1) == 0) {
         if constexpr (G >= 4) {
             if (nt)
-                hipLaunchKernelGGL((csum_batch_kernel<G, U, S, true>), grid, block, 0, st, a);
+                hipLaunchKernelGGL((csum_batch_kernel<G, U, S, true>), grid, block, lds, st, a);
             else
-                hipLaunchKernelGGL((csum_batch_kernel<G, U, S, false>), grid, block, 0, st, a);
+                hipLaunchKernelGGL((csum_batch_kernel<G, U, S, false>), grid, block, lds, st, a);
         } else {
             return RNS_E_INVALID;
         }
     } else if (variant & 8) {  // rounds kernel, every round in flight (tiny packets)
         if constexpr (G <= 8 && U <= 2) {
             if (nt && buf)
-                hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, true, G>), grid, block, 0, st, a);
+                hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, true, G>), grid, block, lds, st, a);
             else if (nt)
-                hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, false, G>), grid, block, 0, st, a);
+                hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, false, G>), grid, block, lds, st, a);
             else if (buf)
-                hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, false, true, G>), grid, block, 0, st, a);
+                hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, false, true, G>), grid, block, lds, st, a);
             else
-                hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, false, false, G>), grid, block, 0, st, a);
+                hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, false, false, G>), grid, block, lds, st, a);
         } else {
             return RNS_E_INVALID;
         }
     } else {
         if (nt && buf)
-            hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, true>), grid, block, 0, st, a);
+            hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, true>), grid, block, lds, st, a);
         else if (nt)
-            hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, false>), grid, block, 0, st, a);
+            hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, false>), grid, block, lds, st, a);
         else if (buf)
-            hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, false, true>), grid, block, 0, st, a);
+            hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, false, true>), grid, block, lds, st, a);
         else
-            hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, false, false>), grid, block, 0, st, a);
+            hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, false, false>), grid, block, lds, st, a);
     }
     return hip_status(hipGetLastError());
 }
@@ -1262,7 +1267,8 @@ int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipSt
 template <bool S>
 int dispatch(const CsumArgs &a, uint32_t variant, uint32_t G, uint32_t U, uint32_t max_blocks, hipStream_t st)
 {
-    if (variant > 15 || ((variant & 8) && (variant & 5) != 1))  // bit 3 (deep prefetch): rounds kernel only
+    const uint32_t v = variant & 0xffu;  // bits 8-11: occupancy cap (launch_shape)
+    if (v > 15 || (variant >> 12) || ((v & 8) && (v & 5) != 1))  // bit 3 (deep prefetch): rounds kernel only
         return RNS_E_INVALID;
     if (variant & 4)  // the mixed kernel picks its own per-class shapes
         return launch_shape<64, 4, S>(a, variant, max_blocks, st);

@@ -57,7 +57,13 @@ __global__ __launch_bounds__(256) void read_store(uint8_t *arena, uint32_t n, ui
     if (p0 >= n)
         return;
     const uint32_t np = min(64u, n - static_cast<uint32_t>(p0));
-    const uint64_t b0 = p0 * stride, nch = (static_cast<uint64_t>(np) * stride) >> 4;
+    uint64_t b0 = p0 * stride;
+    if constexpr (MODE == 6) {  // a dependent per-wave descriptor load before the slab (always 0 here)
+        const uint64_t dep = reinterpret_cast<const uint64_t *>(out)[(p0 + lane) % n / 4];
+        b0 += __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(dep & 0));
+        b0 += static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(dep)) == 0x7fffffffu);
+    }
+    const uint64_t nch = (static_cast<uint64_t>(np) * stride) >> 4;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(arena + b0, 0, static_cast<int>(nch * 16), 0x00020000);
     const uint32_t fch = 16 / 16, sch = stride / 16;  // the field's chunk within a packet; chunks per packet
     uint32_t acc = 0;
@@ -100,12 +106,12 @@ __global__ __launch_bounds__(256) void read_store(uint8_t *arena, uint32_t n, ui
         if (pend)
             *reinterpret_cast<u32x4 *>(arena + b0 + pc * 16) = pv;
     }
-    if constexpr (MODE >= 4)
+    if constexpr (MODE == 4 || MODE == 5)
         return;
     if (lane >= np)
         return;
     const uint64_t f = (p0 + lane) * stride + 16;
-    if constexpr (MODE == 0) {
+    if constexpr (MODE == 0 || MODE == 6) {
         if (acc == 0x12345678u)
             out[p0 + lane] = 1;
     } else if constexpr (MODE == 1) {
@@ -149,7 +155,8 @@ int main(int argc, char **argv)
     uint8_t *arena;
     uint16_t *out;
     CHECK(hipMalloc(&arena, bytes + 256));
-    CHECK(hipMalloc(&out, static_cast<size_t>(n) * 2));
+    CHECK(hipMalloc(&out, static_cast<size_t>(n) * 2 + 64));
+    CHECK(hipMemset(out, 0, static_cast<size_t>(n) * 2 + 64));
     CHECK(hipMemset(arena, 0x5a, bytes));
     const int iters = 20;
     const uint32_t sblocks = (n + 255) / 256, rblocks = (n + 255) / 256;  // read: 4 waves of 64 packets per block
@@ -170,6 +177,11 @@ int main(int argc, char **argv)
         report("read+store2", time_ms([&] { read_store<1><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
         report("read+store32", time_ms([&] { read_store<2><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
         report("read+compact", time_ms([&] { read_store<3><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read+dep_desc", time_ms([&] { read_store<6><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        // occupancy capped by dynamic LDS per 4-wave workgroup (160 KB per CU)
+        report("read_occ4", time_ms([&] { read_store<0><<<rblocks, 256, 40 << 10>>>(arena, n, stride, out); }, iters));
+        report("read_occ3", time_ms([&] { read_store<0><<<rblocks, 256, 52 << 10>>>(arena, n, stride, out); }, iters));
+        report("read_occ2", time_ms([&] { read_store<0><<<rblocks, 256, 80 << 10>>>(arena, n, stride, out); }, iters));
         report("read+inline16", time_ms([&] { read_store<4><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
         report("read+deferred16", time_ms([&] { read_store<5><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
         report("read_plain", time_ms([&] { read_store<0, 0><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
