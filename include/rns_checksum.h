@@ -165,6 +165,22 @@ int rns_rx_verify_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64
                       uint32_t n, const uint8_t *local_ipv4, const uint8_t *local_ipv6, uint8_t *d_status,
                       uint16_t *d_l4_sum, void *stream);
 
+/* Transmit finalize (SURVEY a6, §8f row 2 for whole datagrams): for each finished
+ * outgoing IP datagram d_arena[d_off[i] .. + d_len[i]), the checksums the stack's
+ * transmit path stores — tcp_output (tcp.rs:957-973: pseudo-header from the header's
+ * source and destination, length as u16, field [16..18] of the segment), udp_output
+ * (udp.rs:151-171, [6..8], 0 stored as is), icmp_output_v4 (icmp.rs:87-95, [2..4], no
+ * pseudo-header), icmp_output_v6 (icmp.rs:97-112, [2..4], full length, protocol 58) and
+ * ip_output_v4 (ip.rs:140-160, header[10..12] over IHL*4 bytes) — computed as if the
+ * fields were zero (alloc_header zero-fills them, buf.rs:286-288) and stored big-endian
+ * in place, with every pseudo-header formed on the device.  One pass over each
+ * datagram's bytes.  Datagrams must not overlap.  d_status (optional) gets RNS_TX_*. */
+#define RNS_TX_IP_FILLED      0x01u  /* IPv4 header checksum stored */
+#define RNS_TX_L4_FILLED      0x02u  /* TCP / UDP / ICMP checksum stored */
+#define RNS_TX_MALFORMED      0x80u  /* bad version / IHL / too short, or outside the arena: untouched */
+int rns_tx_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off, const uint32_t *d_len,
+                    uint32_t n, uint8_t *d_status, void *stream);
+
 /* Tuning entry (bench / tests): explicit kernel shape.  variant bit 0: 0 = group
  * kernel (one lane stores each result), 1 = rounds kernel (a wave owns 64
  * consecutive packets, one coalesced result store); bit 1: nontemporal packet

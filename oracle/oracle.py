@@ -153,6 +153,71 @@ def rx_verify_ref(pkt: bytes, local4: bytes, local6: bytes, ones_comp=None) -> t
     return st, l4
 
 
+TX_IP_FILLED = 0x01
+TX_L4_FILLED = 0x02
+TX_MALFORMED = 0x80
+
+
+def tx_fill_ref(pkt: bytes, ones_comp=None) -> tuple:
+    """(datagram bytes, status bits) after the reference's transmit path has filled the
+    checksums of one finished datagram — the fields are computed as zero, as
+    alloc_header leaves them (buf.rs:286-288), whatever they hold on input:
+
+    tcp_output (tcp.rs:957-973): pseudo-header (source = the local address = the
+    header's source, dest, length = segment length as u16, 6), then
+    compute_buffer_ones_comp(ph, segment) ^ 0xffff at segment[16..18];
+    udp_output (udp.rs:151-171): the same with protocol 17 at [6..8] (a result of 0 is
+    stored as is); icmp_output_v4 (icmp.rs:87-95): compute_buffer_ones_comp(0, segment)
+    ^ 0xffff at [2..4]; icmp_output_v6 (icmp.rs:97-112): pseudo-header with the full
+    segment length, protocol 58, at [2..4]; ip_output_v4 (ip.rs:140-160):
+    compute_checksum(header) at header[10..12] (the reference always sends IHL 5; IHL*4
+    bytes here).  Datagrams the reference cannot produce (bad version, IHL < 5, short
+    buffers) are TX_MALFORMED and left unchanged; protocols it does not checksum, or a
+    segment too short for its field, get no L4 fill.
+    """
+    oc = ones_comp or ones_comp_py
+    p = bytearray(pkt)
+    L = len(p)
+    if L == 0:
+        return bytes(p), TX_MALFORMED
+    version = p[0] >> 4
+    if version == 4:
+        hdr = (p[0] & 0xF) * 4
+        if hdr < 20 or hdr > L:
+            return bytes(p), TX_MALFORMED
+        proto, src, dst = p[9], bytes(p[12:16]), bytes(p[16:20])
+    elif version == 6:
+        hdr = 40
+        if L < 40:
+            return bytes(p), TX_MALFORMED
+        proto, src, dst = p[6], bytes(p[8:24]), bytes(p[24:40])
+    else:
+        return bytes(p), TX_MALFORMED
+    seg_len = L - hdr
+    field, seed = None, 0
+    if proto == 6:
+        field, seed = 16, pseudo_header_py(src, dst, seg_len & 0xFFFF, 6)
+    elif proto == 17:
+        field, seed = 6, pseudo_header_py(src, dst, seg_len & 0xFFFF, 17)
+    elif proto == 1 and version == 4:
+        field = 2
+    elif proto == 58 and version == 6:
+        field, seed = 2, pseudo_header_py(src, dst, seg_len, 58)
+    st = 0
+    if field is not None and seg_len >= field + 2:
+        f = hdr + field
+        p[f:f + 2] = b"\x00\x00"
+        c = oc(seed, bytes(p[hdr:])) ^ 0xFFFF
+        p[f:f + 2] = c.to_bytes(2, "big")
+        st |= TX_L4_FILLED
+    if version == 4:
+        p[10:12] = b"\x00\x00"
+        c = oc(0, bytes(p[:hdr])) ^ 0xFFFF
+        p[10:12] = c.to_bytes(2, "big")
+        st |= TX_IP_FILLED
+    return bytes(p), st
+
+
 # --------------------------------------------------------------------------
 # deterministic synthetic bytes: splitmix64 (SURVEY §8d, seed 0x5EED_C0DE)
 # --------------------------------------------------------------------------

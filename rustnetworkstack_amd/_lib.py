@@ -31,6 +31,9 @@ RNS_RX_FRAGMENT = 0x08
 RNS_RX_UNKNOWN_PROTO = 0x10
 RNS_RX_ACCEPT = 0x40
 RNS_RX_MALFORMED = 0x80
+RNS_TX_IP_FILLED = 0x01
+RNS_TX_L4_FILLED = 0x02
+RNS_TX_MALFORMED = 0x80
 
 # Every symbol include/rns_checksum.h declares (tests/test_abi.py checks the header,
 # this list and the library's dynamic symbol table agree).
@@ -45,6 +48,7 @@ EXPORTED_SYMBOLS = (
     "rns_csum_chain_dev",
     "rns_csum_fill_dev",
     "rns_rx_verify_dev",
+    "rns_tx_fill_dev",
     "rns_host_ctx_create",
     "rns_host_ctx_destroy",
     "rns_csum_batch_host",
@@ -111,6 +115,7 @@ _SIGNATURES = {
     "rns_csum_chain_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp]),
     "rns_csum_fill_dev": (_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u32, _vp, _u32, _u32, _vp, _vp]),
     "rns_rx_verify_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),
+    "rns_tx_fill_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp]),
     "rns_host_ctx_create": (_int, [_int, _u64, _u32, ctypes.POINTER(_vp)]),
     "rns_host_ctx_destroy": (_int, [_vp]),
     "rns_csum_batch_host": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32]),

@@ -258,6 +258,32 @@ def rx_verify(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, loca
     return status
 
 
+def tx_fill(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, *,
+            status: torch.Tensor | None = None) -> torch.Tensor:
+    """Transmit finalize of a batch of outgoing IP datagrams (rns_tx_fill_dev): the
+    IPv4 header checksum and the TCP / UDP / ICMP checksum of every datagram stored in
+    place, pseudo-headers formed on the device (tcp.rs:957-973, udp.rs:151-171,
+    icmp.rs:87-112, ip.rs:140-160).  Returns a uint8 status per datagram (RNS_TX_*)."""
+    _require_cuda(arena, "arena", (torch.uint8,))
+    _require_cuda(off, "off", (torch.int64,))
+    _require_cuda(length, "length", (torch.int32,))
+    n = off.numel()
+    if length.numel() != n:
+        raise ValueError("off and length must have the same number of datagrams")
+    dev = arena.device
+    if status is None:
+        status = torch.empty(n, dtype=torch.uint8, device=dev)
+    else:
+        _require_cuda(status, "status", (torch.uint8,))
+        if status.numel() != n:
+            raise ValueError("status must have one entry per datagram")
+    with torch.cuda.device(dev):
+        st = _lib.load().rns_tx_fill_dev(arena.data_ptr(), arena.numel(), off.data_ptr(), length.data_ptr(), n,
+                                        status.data_ptr(), _stream_handle(dev))
+    _lib.check(st, "rns_tx_fill_dev")
+    return status
+
+
 def fill_splitmix64(buf: torch.Tensor, seed: int) -> torch.Tensor:
     """Fill a device uint8 buffer with the splitmix64 byte stream (same bytes as
     oracle.splitmix64_bytes(seed, n))."""

@@ -258,7 +258,7 @@ __host__ __device__ __forceinline__ uint64_t buf_records(const CsumArgs &a) { re
 // chunks their finish needs (a datagram's header, a packet's checksum field) are
 // copied to LDS by the lanes that load them anyway, and the owner lane finishes
 // from there: no extra memory round, no per-chunk header/field masking.
-enum StashMode : int { kStashNone = 0, kStashHead = 1, kStashField = 2 };
+enum StashMode : int { kStashNone = 0, kStashHead = 1, kStashField = 2, kStashTx = 3 };
 // Chunks stashed per packet: a datagram's first 5 chunks hold its first
 // 16*5 - 15 = 65 >= 60 bytes (the longest IPv4 header) at any start offset; a
 // field's chunks are the 32-byte sector that holds its first byte plus the next
@@ -273,7 +273,7 @@ constexpr int kFieldBlock = RNS_FILL_BLOCK;
 constexpr int kFieldChunks = kFieldBlock / 16;
 static_assert(kFieldBlock >= 32 && kFieldBlock <= 128 && (kFieldBlock & (kFieldBlock - 1)) == 0, "fill block");
 template <int MODE>
-constexpr int kStashChunks = MODE == kStashHead ? 5 : MODE == kStashField ? kFieldChunks + 1 : 0;
+constexpr int kStashChunks = MODE == kStashHead ? 5 : MODE == kStashField ? kFieldChunks + 1 : MODE == kStashTx ? 6 : 0;
 
 // First stashed chunk (relative to the packet's chunk 0) for a field whose first
 // byte is in chunk cf: the chunk that starts the field's aligned kFieldBlock-byte
@@ -927,18 +927,18 @@ constexpr int kMixedBlock = STASH ? 64 : kBlock;
 // folds, and stores the (complemented) result into the field big-endian (set_be16,
 // util.rs:132-135) after the whole wave has read its 64 packets.
 // RX: receive verify (see above).
-template <bool STRIDED, bool NT, bool BUF, bool FILL, bool RX = false>
+template <bool STRIDED, bool NT, bool BUF, bool FILL, bool RX = false, bool TX = false>
 #ifndef RNS_MIXED_OCC
 #define RNS_MIXED_OCC 4
 #endif
-__global__ __launch_bounds__(kMixedBlock<FILL || RX>, (BUF && !FILL && !RX) ? RNS_MIXED_OCC : 3) void csum_mixed_kernel(const CsumArgs a)
+__global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX && !TX) ? RNS_MIXED_OCC : 3) void csum_mixed_kernel(const CsumArgs a)
 {
-    static_assert(!(FILL && RX) && !(STRIDED && RX), "one mode at a time");
-    constexpr int kMode = RX ? kStashHead : FILL ? kStashField : kStashNone;
+    static_assert(int(FILL) + int(RX) + int(TX) <= 1 && !(STRIDED && (RX || TX)), "one mode at a time");
+    constexpr int kMode = RX ? kStashHead : FILL ? kStashField : TX ? kStashTx : kStashNone;
     constexpr int kNS = kStashChunks<kMode>;
     constexpr uint32_t kPer = 64;  // packets per wave batch
     // per wave: kNS chunks for each of its 64 packets, indexed by sorted position
-    constexpr int BLK = kMixedBlock<FILL || RX>;
+    constexpr int BLK = kMixedBlock<FILL || RX || TX>;
     __shared__ uint4 stash_lds[kNS ? (BLK / 64) * kPer * kNS : 1];
     uint4 *const st = stash_lds + (threadIdx.x >> 6) * (kPer * kNS);
     const uint32_t lane = threadIdx.x & 63;
@@ -1023,6 +1023,117 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX>, (BUF && !FILL && !RX) ? RN
             RNS_RUN_CLASS(5 % kNumClasses);
 #undef RNS_RUN_CLASS
 
+        if constexpr (TX) {
+            // Transmit finalize: mine = the whole datagram's word sum.  From the stash
+            // (chunks 0-5: >= 81 bytes past any start offset): parse the header, sum the
+            // IPv4 header H and take the L4 segment as mine - H; both fields count as zero.
+            const uint4 *own = st + pos * kNS;
+            wave_lds_fence();  // the stash was written by other lanes of this wave
+            const uint32_t s = static_cast<uint32_t>(d_start & 15);
+            uint8_t status = RNS_TX_MALFORMED;
+            uint32_t ipf = 0xFFFFFFFFu, l4f = 0xFFFFFFFFu;  // field offsets in the datagram (none)
+            uint32_t ipc = 0, l4c = 0;
+            if (live && d_len != 0) {
+                const uint8_t *b = reinterpret_cast<const uint8_t *>(own) + s;  // datagram byte i = b[i], i < 96 - s
+                const uint32_t version = b[0] >> 4;
+                uint32_t hdr = 0, proto = 0, field = 0xFFFFFFFFu, seed = 0;
+                bool ok = false;
+                const uint32_t L = d_len;
+                auto be16 = [&](uint32_t i) { return (static_cast<uint32_t>(b[i]) << 8) | b[i + 1]; };
+                if (version == 4) {
+                    hdr = (b[0] & 0xFu) * 4u;
+                    ok = hdr >= 20 && hdr <= L;
+                    proto = b[9];
+                } else if (version == 6) {
+                    hdr = 40;
+                    ok = L >= 40;
+                    proto = b[6];
+                }
+                if (ok) {
+                    const uint32_t seg = L - hdr;
+                    uint32_t addr = 0;  // BE word sum of source + destination (tcp.rs:958-966: local = header source)
+                    if (version == 4) {
+                        for (uint32_t i = 12; i < 20; i += 2)
+                            addr += be16(i);
+                    } else {
+                        for (uint32_t i = 8; i < 40; i += 2)
+                            addr += be16(i);
+                    }
+                    const uint32_t l16 = seg & 0xFFFFu;  // packet.len() as u16 (tcp.rs:942, udp.rs:152)
+                    if (proto == 6 || proto == 17) {
+                        field = proto == 6 ? 16u : 6u;
+                        seed = fold16(addr + proto + l16);  // v4: len16; v6: len32 whose high half is 0
+                    } else if (proto == 1 && version == 4) {
+                        field = 2;  // icmp_output_v4: no pseudo-header
+                    } else if (proto == 58 && version == 6) {
+                        field = 2;  // icmp_output_v6: full length, protocol 58
+                        seed = fold16(addr + 58 + (seg >> 16) + (seg & 0xFFFFu));
+                    }
+                    status = 0;
+                    // header sum (<= 60 bytes, chunks 0-4) and the fields' own words
+                    uint4 ch[5];
+#pragma unroll
+                    for (int i = 0; i < 5; ++i)
+                        ch[i] = own[i];
+                    const int hlo = static_cast<int>(s), hhi = hlo + static_cast<int>(hdr);
+                    const uint32_t H = stash_sum_le(ch, hlo, hhi);
+                    // a field's two bytes, as the LE words (aligned pairing) or BE words (packet pairing) hold them
+                    auto le_contrib = [&](uint32_t f) {
+                        const uint32_t b0 = b[f], b1 = b[f + 1];
+                        return ((s + f) & 1) ? (b0 << 8) + b1 : b0 + (b1 << 8);
+                    };
+                    if (version == 4) {  // ip_output_v4 (ip.rs:158-159): over the header, [10..12] as zero
+                        ipf = 10;
+                        ipc = finalize_bits(H - le_contrib(10), odd, false, 0u, true, RNS_FLAG_COMPLEMENT);
+                        status |= RNS_TX_IP_FILLED;
+                    }
+                    if (field != 0xFFFFFFFFu && seg >= field + 2) {
+                        l4f = hdr + field;
+                        uint32_t l4 = mine - H - le_contrib(l4f);
+                        if (big) {  // > 128 KiB: the exact big-endian sums mod 2^32
+                            const uint32_t b0 = b[l4f], b1 = b[l4f + 1];
+                            l4 = mine - stash_sum_be(ch, hlo, hhi, odd) - ((b0 << 8) + b1);  // l4f even: a BE word
+                        }
+                        l4c = finalize_bits(l4, odd, big, seed, true, RNS_FLAG_COMPLEMENT);
+                        status |= RNS_TX_L4_FILLED;
+                    }
+                }
+            }
+            if (live && a.status)
+                a.status[p] = status;
+            // store the fields: patch the stash, then rewrite each field's 32-byte memory
+            // sector from it when the sector lies inside the datagram and the stash, else
+            // store the two bytes (set_be16, util.rs:132-135)
+            uint8_t *own_b = reinterpret_cast<uint8_t *>(st + pos * kNS);
+            uint8_t *arena_w = const_cast<uint8_t *>(a.arena);
+            const uint32_t fld[2] = {ipf, l4f}, val[2] = {ipc, l4c};
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                if (fld[k] != 0xFFFFFFFFu) {
+                    own_b[s + fld[k]] = static_cast<uint8_t>(val[k] >> 8);
+                    own_b[s + fld[k] + 1] = static_cast<uint8_t>(val[k]);
+                }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (fld[k] == 0xFFFFFFFFu)
+                    continue;
+                const uint32_t fpos = s + fld[k];  // from chunk 0's first byte
+                const int lo = static_cast<int>(fpos >> 4) -
+                               static_cast<int>((arena_parity(a) + static_cast<uint32_t>(d_start >> 4) + (fpos >> 4)) & 1u);
+                const uint64_t sec = d_start - s + static_cast<uint64_t>(16 * static_cast<int64_t>(lo));
+                const bool whole = lo >= 0 && lo + 2 <= kNS && sec >= d_start && sec + 32 <= d_start + d_len &&
+                                   (fpos - 16u * static_cast<uint32_t>(lo)) != 31u;
+                if (whole) {
+                    uint4 *sp = reinterpret_cast<uint4 *>(arena_w + sec);
+                    sp[0] = own[lo];
+                    sp[1] = own[lo + 1];
+                } else {
+                    arena_w[d_start + fld[k]] = static_cast<uint8_t>(val[k] >> 8);
+                    arena_w[d_start + fld[k] + 1] = static_cast<uint8_t>(val[k]);
+                }
+            }
+            continue;
+        }
         if constexpr (RX) {
             // mine = the whole datagram's word sum T.  Header H from the stash (seed 0,
             // <= 60 bytes); L4 = T - H, seeded with the pseudo-header sum.  Both parts
@@ -1554,6 +1665,33 @@ int rns_rx_verify_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64
         hipLaunchKernelGGL((csum_mixed_kernel<false, kNT, true, false, true>), grid, block, 0, st, a);
     else
         hipLaunchKernelGGL((csum_mixed_kernel<false, kNT, false, false, true>), grid, block, 0, st, a);
+    return hip_status(hipGetLastError());
+}
+
+int rns_tx_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off, const uint32_t *d_len,
+                    uint32_t n, uint8_t *d_status, void *stream)
+{
+    if (n == 0)
+        return RNS_OK;
+    if (!d_arena || !d_off || !d_len)
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    CsumArgs a{};
+    set_arena(a, d_arena, arena_bytes);
+    a.off = d_off;
+    a.len = d_len;
+    a.n = n;
+    a.flags = RNS_FLAG_COMPLEMENT;
+    a.status = d_status;
+    constexpr int BLK = kMixedBlock<true>;
+    const uint64_t waves = (static_cast<uint64_t>(n) + 63) / 64;  // 64 datagrams per wave
+    const dim3 grid(static_cast<uint32_t>((waves + BLK / 64 - 1) / (BLK / 64))), block(BLK);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (buf_records(a) < kOobOffset)
+        hipLaunchKernelGGL((csum_mixed_kernel<false, false, true, false, false, true>), grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL((csum_mixed_kernel<false, false, false, false, false, true>), grid, block, 0, st, a);
     return hip_status(hipGetLastError());
 }
 

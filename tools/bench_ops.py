@@ -6,6 +6,8 @@ batch checksum, on the headline batch (2^20 x 1500 B) and on IMIX:
              IP trim, three fragments [492, 512, 496]
 * fill     — rns_csum_fill_dev: transmit fill of the TCP checksum field [16..18]
 * verify   — rns_rx_verify_dev: IPv4 header + TCP checks of whole datagrams
+* tx       — rns_tx_fill_dev: IPv4 header + TCP checksums of whole datagrams stored in
+             place, pseudo-headers formed on the device
 
 Timing: one pair of HIP events around K back-to-back launches on the launch stream,
 median of R rounds.  GB/s counts algorithmic bytes (payload read + result bytes
@@ -23,7 +25,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from rustnetworkstack_amd.batch import (PreparedBatch, csum_chain, csum_fill, rx_verify)  # noqa: E402
+from rustnetworkstack_amd.batch import (PreparedBatch, csum_chain, csum_fill, rx_verify, tx_fill)  # noqa: E402
 from rustnetworkstack_amd.workloads import DeviceBatch, make_layout  # noqa: E402
 
 L4 = bytes([192, 168, 1, 2])
@@ -75,7 +77,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--configs", default="c3_1500B,c5_imix")
-    ap.add_argument("--ops", default="csum,chain,fill,verify")
+    ap.add_argument("--ops", default="csum,chain,fill,verify,tx")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     ops = set(args.ops.split(","))
@@ -96,6 +98,13 @@ def main():
         if "fill" in ops:
             ms = timed(lambda: csum_fill(b.arena, b.off, b.length, b.seed, field_off=16), args.steps, args.rounds)
             r["fill"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1)}
+        if "tx" in ops:
+            write_ipv4_tcp_headers(b, lay, dev)
+            st = torch.empty(n, dtype=torch.uint8, device=dev)
+            ms = timed(lambda: tx_fill(b.arena, b.off, b.length, status=st), args.steps, args.rounds)
+            filled = int((st == 3).sum().item())
+            r["tx"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + n) / ms / 1e6, 1), "filled": filled,
+                       "packets": n}
         if "verify" in ops:
             # turn every packet into a valid IPv4/TCP datagram first (header written
             # on the GPU, IPv4 and TCP checksums filled), so every byte is checked
