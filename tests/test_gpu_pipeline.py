@@ -41,3 +41,44 @@ def test_socket_to_verdicts(oracle):
     b.close()
     assert np.array_equal(np.concatenate(got_len), lens[nonempty])
     assert np.array_equal(np.concatenate(got_st), expect)
+
+
+def test_tx_pipeline_to_socket(oracle):
+    """Datagrams with unset checksum fields in pinned slots -> TxPipeline -> socket; the
+    other end receives exactly what the reference's transmit path would send."""
+    from rustnetworkstack_amd.batch import recv_batch
+    from rustnetworkstack_amd.pipeline import TxPipeline
+    from test_gpu_tx import outgoing
+    pkts = [p for p in outgoing(5000, 0x5E4D) if 0 < len(p) <= 2048]
+    want = [O.tx_fill_ref(p, ones_comp=oracle.compute_ones_comp) for p in pkts]
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+    for s_, opt in ((a, socket.SO_SNDBUF), (b, socket.SO_RCVBUF)):
+        s_.setsockopt(socket.SOL_SOCKET, opt, 32 << 20)
+    received = []
+
+    def drain():
+        buf = np.empty(2048 * 1024, dtype=np.uint8)
+        while len(received) < len(pkts):
+            off, ln = recv_batch(b.fileno(), buf, 2048, 1024, timeout_ms=5000)
+            if ln.shape[0] == 0:
+                return
+            received.extend(buf[int(o):int(o) + int(n)].tobytes() for o, n in zip(off, ln))
+
+    t = threading.Thread(target=drain)
+    t.start()
+    pipe = TxPipeline(device=0, max_pkts=1024)
+    statuses = []
+    for i0 in range(0, len(pkts), 1024):
+        chunk = pkts[i0:i0 + 1024]
+        slots = pipe.slots()
+        for k, p in enumerate(chunk):
+            slots[k, :len(p)] = np.frombuffer(p, dtype=np.uint8)
+        statuses.append(pipe.send(a.fileno(), np.array([len(p) for p in chunk], dtype=np.uint32)))
+    t.join(timeout=60)
+    pipe.close()
+    a.close()
+    b.close()
+    assert np.array_equal(np.concatenate(statuses), np.array([w[1] for w in want], dtype=np.uint8))
+    assert len(received) == len(pkts)
+    bad = [i for i in range(len(pkts)) if received[i] != want[i][0]]
+    assert not bad, bad[:5]

@@ -1,10 +1,14 @@
-"""End-to-end batched receive rate: a sender thread writes N valid IPv4/TCP datagrams
-(1500 B) into a SOCK_SEQPACKET socketpair (TUN-like: one datagram per read); the
-receiver runs RxPipeline (rns_io_recv_batch into pinned 2048-B slots -> H2D ->
-fused rns_rx_verify_dev -> verdicts D2H) until all arrived.  Reports packets/s and
-GB/s of datagram bytes, and the share of time in each stage.
+"""End-to-end batched receive / transmit rates over a SOCK_SEQPACKET socketpair
+(TUN-like: one datagram per read / write).
 
-    python tools/bench_pipeline.py [--packets 262144] [--batch 8192]
+Receive (default): a sender thread writes N valid IPv4/TCP datagrams (1500 B); the
+receiver runs RxPipeline (rns_io_recv_batch into pinned 2048-B slots -> H2D -> fused
+rns_rx_verify_dev -> verdicts D2H) until all arrived.
+Transmit (--tx): the same datagrams with their checksum fields zeroed are placed in
+TxPipeline's pinned slots and sent (H2D -> rns_tx_fill_dev -> header bytes D2H ->
+rns_io_send_batch); a drain thread reads them and the result is spot-checked.
+
+    python tools/bench_pipeline.py [--packets 262144] [--batch 8192] [--tx]
 """
 import argparse
 import json
@@ -20,7 +24,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from rustnetworkstack_amd.batch import send_batch  # noqa: E402
-from rustnetworkstack_amd.pipeline import RxPipeline  # noqa: E402
+from rustnetworkstack_amd.batch import recv_batch  # noqa: E402
+from rustnetworkstack_amd.pipeline import RxPipeline, TxPipeline  # noqa: E402
 from rustnetworkstack_amd.workloads import DeviceBatch, make_layout  # noqa: E402
 from bench_ops import L4, L6, write_ipv4_tcp_headers  # noqa: E402
 
@@ -30,7 +35,10 @@ def main():
     ap.add_argument("--packets", type=int, default=1 << 18)
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--out", default="")
+    ap.add_argument("--tx", action="store_true")
     args = ap.parse_args()
+    if args.tx:
+        return main_tx(args)
     dev = torch.device("cuda:0")
     lay = make_layout("c3_1500B", n=args.packets)
     b = DeviceBatch(lay, dev)
@@ -58,6 +66,59 @@ def main():
            "seconds": round(dt, 3), "packets_per_s": round(got / dt), "GBps": round(got * 1500 / dt / 1e9, 3),
            "path": "AF_UNIX SOCK_SEQPACKET socketpair (TUN-like) -> rns_io_recv_batch (2048-B slots, pinned) -> "
                    "H2D -> rns_rx_verify_dev -> status D2H; sender on another host thread"}
+    print(json.dumps(res))
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(res, f, indent=1)
+    pipe.close()
+
+
+def main_tx(args):
+    dev = torch.device("cuda:0")
+    lay = make_layout("c3_1500B", n=args.packets)
+    b = DeviceBatch(lay, dev)
+    write_ipv4_tcp_headers(b, lay, dev)          # valid datagrams, built on the GPU
+    good = b.arena[:lay.arena_bytes].cpu().numpy()
+    del b
+    n = lay.n
+    dgrams = good[(lay.off.reshape(-1, 1) + np.arange(1500, dtype=np.uint64)).reshape(-1)].reshape(n, 1500)
+    unfilled = dgrams.copy()
+    unfilled[:, 10:12] = 0                       # what ip_output_v4 / tcp_output see before their checksums
+    unfilled[:, 36:38] = 0
+    a, r = socket.socketpair(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+    for s_, opt in ((a, socket.SO_SNDBUF), (r, socket.SO_RCVBUF)):
+        s_.setsockopt(socket.SOL_SOCKET, opt, 64 << 20)
+    pipe = TxPipeline(device=0, max_pkts=args.batch)
+    got = [0]
+    sample = {}
+
+    def drain():
+        buf = np.empty(2048 * 4096, dtype=np.uint8)
+        while got[0] < n:
+            off, ln = recv_batch(r.fileno(), buf, 2048, 4096, timeout_ms=5000)
+            if ln.shape[0] == 0:
+                return
+            for k in range(0, ln.shape[0], 997):   # spot-check every 997th datagram
+                sample[got[0] + k] = buf[int(off[k]):int(off[k]) + int(ln[k])].copy()
+            got[0] += ln.shape[0]
+
+    t = threading.Thread(target=drain)
+    t0 = time.perf_counter()
+    t.start()
+    filled = 0
+    for i0 in range(0, n, args.batch):
+        k = min(args.batch, n - i0)
+        pipe.slots()[:k, :1500] = unfilled[i0:i0 + k]
+        st = pipe.send(a.fileno(), np.full(k, 1500, dtype=np.uint32))
+        filled += int((st == 3).sum())
+    t.join()
+    dt = time.perf_counter() - t0
+    exact = all(np.array_equal(v, dgrams[i]) for i, v in sample.items())
+    res = {"direction": "transmit", "packets": n, "received": got[0], "filled": filled,
+           "sample_exact": exact, "sampled": len(sample), "seconds": round(dt, 3),
+           "packets_per_s": round(got[0] / dt), "GBps": round(got[0] * 1500 / dt / 1e9, 3),
+           "path": "host datagrams -> pinned 2048-B slots -> H2D -> rns_tx_fill_dev -> 128 B/slot D2H -> "
+                   "rns_io_send_batch -> AF_UNIX SOCK_SEQPACKET socketpair; drain on another host thread"}
     print(json.dumps(res))
     if args.out:
         with open(args.out, "w") as f:
