@@ -68,6 +68,13 @@ struct CsumArgs {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// Cache-policy bits of the "nontemporal" buffer loads (gfx950 CPol: 1 = sc0, 2 = nt,
+// 16 = sc1).  A/B knob: -DRNS_NT_AUX=...
+#ifndef RNS_NT_AUX
+#define RNS_NT_AUX 2
+#endif
+constexpr int kNtAux = RNS_NT_AUX;
+
 // One 16-byte chunk.  NT = nontemporal (streamed once: do not keep it in the
 // caches; the HBM read probe in tools/ measured +5..10 % for streaming reads).
 template <bool NT>
@@ -358,7 +365,7 @@ __device__ __forceinline__ void issue_pass(const CsumArgs &a, __amdgpu_buffer_rs
         const bool in = c < k.nch;
         if constexpr (BUF) {
             const uint32_t off = in ? static_cast<uint32_t>(first + (static_cast<uint64_t>(c) << 4)) : kOobOffset;
-            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, NT ? 2 : 0);
+            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, NT ? kNtAux : 0);
             v[u] = make_uint4(x.x, x.y, x.z, x.w);
         } else {
             const uint8_t *ptr = a.arena + first + (in ? (static_cast<uint64_t>(c) << 4) : 0);
@@ -661,7 +668,7 @@ __device__ __forceinline__ Pkt prefetch_class(const CsumArgs &a, __amdgpu_buffer
         const bool in = static_cast<uint32_t>(u) < U && c < k.nch;
         if constexpr (BUF) {
             const uint32_t o = in ? static_cast<uint32_t>(first + (static_cast<uint64_t>(c) << 4)) : kOobOffset;
-            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, NT ? 2 : 0);
+            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, NT ? kNtAux : 0);
             w[u] = make_uint4(x.x, x.y, x.z, x.w);
         } else {
             const uint4 x = load_chunk<NT>(a.arena + first + (in ? (static_cast<uint64_t>(c) << 4) : 0));
