@@ -9,8 +9,16 @@ The reference handles one packet per loop iteration on its receive thread
 ip.rs:38 -> checks ip.rs:76, tcp.rs:544).  Here one call moves every queued datagram
 (rns_io_recv_batch into 2048-byte MRU slots, netif.rs:66), copies the used slots to
 the GPU in one transfer and verifies them with one kernel (rns_rx_verify_dev).
+
+Both directions also run overlapped (``RxPipeline.stream``, ``TxPipeline.submit`` /
+``complete``): two buffer sets, the GPU work of one batch (H2D, kernel, D2H into
+pinned memory) queued on a private stream while the host reads or writes the
+datagrams of the other.
 """
 from __future__ import annotations
+
+from collections import deque
+from typing import Iterator
 
 import numpy as np
 import torch
@@ -20,6 +28,25 @@ from .batch import PinnedBuffer, recv_batch, rx_verify, send_batch, tx_fill
 MRU = 2048  # netif.rs:66
 
 
+class _Slots:
+    """One buffer set: pinned host slots + lengths + per-slot results, and their HBM twins."""
+
+    def __init__(self, dev: torch.device, max_pkts: int, slot_bytes: int, head: int = 0):
+        self.host = PinnedBuffer(slot_bytes * max_pkts)
+        self.h_len = PinnedBuffer(4 * max_pkts)
+        self.h_status = PinnedBuffer(max_pkts)
+        self.h_head = PinnedBuffer(head * max_pkts) if head else None
+        self.d_arena = torch.empty(slot_bytes * max_pkts, dtype=torch.uint8, device=dev)
+        self.d_len = torch.empty(max_pkts, dtype=torch.int32, device=dev)
+        self.d_status = torch.empty(max_pkts, dtype=torch.uint8, device=dev)
+        self.done = torch.cuda.Event()
+
+    def close(self):
+        for b in (self.host, self.h_len, self.h_status, self.h_head):
+            if b is not None:
+                b.free()
+
+
 class RxPipeline:
     def __init__(self, local_ipv4: bytes, local_ipv6: bytes, device: int = 0, max_pkts: int = 65536,
                  slot_bytes: int = MRU):
@@ -27,34 +54,77 @@ class RxPipeline:
         self.slot = slot_bytes
         self.max_pkts = max_pkts
         self.dev = torch.device(f"cuda:{device}")
-        self.host = PinnedBuffer(slot_bytes * max_pkts)
-        self.h_len = PinnedBuffer(4 * max_pkts)
-        self.d_arena = torch.empty(slot_bytes * max_pkts, dtype=torch.uint8, device=self.dev)
+        self._sets = [_Slots(self.dev, max_pkts, slot_bytes)]
         self.d_off = (torch.arange(max_pkts, dtype=torch.int64, device=self.dev) * slot_bytes).contiguous()
-        self.d_len = torch.empty(max_pkts, dtype=torch.int32, device=self.dev)
-        self.d_status = torch.empty(max_pkts, dtype=torch.uint8, device=self.dev)
+        self._stream = None
+
+    @property
+    def host(self) -> PinnedBuffer:
+        """Set 0's pinned slots: where ``receive`` leaves packet i (slot i)."""
+        return self._sets[0].host
+
+    def _submit(self, s: _Slots, ln: np.ndarray) -> None:
+        """Queue H2D + verify + status D2H of the first len(ln) slots of ``s`` on the
+        current stream; ``s.done`` marks the status landing in pinned memory."""
+        n = ln.shape[0]
+        hl = s.h_len.array.view(np.uint32)[:n]
+        hl[:] = ln
+        # pinned host memory (rns_host_alloc): every copy is a DMA transfer
+        s.d_arena[: n * self.slot].copy_(torch.from_numpy(s.host.array[: n * self.slot]), non_blocking=True)
+        s.d_len[:n].copy_(torch.from_numpy(hl.view(np.int32)), non_blocking=True)
+        rx_verify(s.d_arena, self.d_off[:n], s.d_len[:n], self.local_ipv4, self.local_ipv6, status=s.d_status[:n])
+        torch.from_numpy(s.h_status.array[:n]).copy_(s.d_status[:n], non_blocking=True)
+        s.done.record()
 
     def receive(self, fd: int, timeout_ms: int = 0) -> tuple[np.ndarray, np.ndarray]:
         """One batch: returns (status uint8 [n], lengths uint32 [n]); packet i is in
         slot i of ``self.host.array``."""
-        off, ln = recv_batch(fd, self.host.array, self.slot, self.max_pkts, timeout_ms)
+        s = self._sets[0]
+        off, ln = recv_batch(fd, s.host.array, self.slot, self.max_pkts, timeout_ms)
         n = off.shape[0]
         if n == 0:
             return np.empty(0, dtype=np.uint8), ln
-        hl = self.h_len.array.view(np.uint32)[:n]
-        hl[:] = ln
         with torch.cuda.device(self.dev):
-            # pinned host memory (rns_host_alloc): both copies are DMA transfers
-            self.d_arena[: n * self.slot].copy_(torch.from_numpy(self.host.array[: n * self.slot]), non_blocking=True)
-            self.d_len[:n].copy_(torch.from_numpy(hl.view(np.int32)), non_blocking=True)
-            rx_verify(self.d_arena, self.d_off[:n], self.d_len[:n], self.local_ipv4, self.local_ipv6,
-                      status=self.d_status[:n])
-            status = self.d_status[:n].cpu().numpy()
-        return status, ln
+            self._submit(s, ln)
+            s.done.synchronize()
+        return s.h_status.array[:n].copy(), ln
+
+    def stream(self, fd: int, timeout_ms: int = 0) -> Iterator[tuple[np.ndarray, np.ndarray, np.ndarray]]:
+        """Overlapped receive: yields (status [n], lengths [n], slots [n, slot_bytes])
+        per batch until a read finds nothing within ``timeout_ms``.  While batch k is
+        on the GPU the host reads batch k+1 into the other buffer set; the yielded
+        arrays stay valid until the generator is resumed."""
+        if len(self._sets) == 1:
+            self._sets.append(_Slots(self.dev, self.max_pkts, self.slot))
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(self.dev)
+        pending = None  # (set, lengths) on the GPU
+        k = 0
+        while True:
+            s = self._sets[k]
+            if pending is None:
+                off, ln = recv_batch(fd, s.host.array, self.slot, self.max_pkts, timeout_ms)
+            else:
+                # take what is queued now (no wait), hand the finished batch over, and
+                # only then block for more: the last batch is not held back by the timeout
+                off, ln = recv_batch(fd, s.host.array, self.slot, self.max_pkts, 0)
+                p, pln = pending
+                p.done.synchronize()
+                n = pln.shape[0]
+                yield p.h_status.array[:n], pln, p.host.array[: n * self.slot].reshape(n, self.slot)
+                pending = None
+                if off.shape[0] == 0:
+                    off, ln = recv_batch(fd, s.host.array, self.slot, self.max_pkts, timeout_ms)
+            if off.shape[0] == 0:
+                return
+            with torch.cuda.device(self.dev), torch.cuda.stream(self._stream):
+                self._submit(s, ln)
+            pending = (s, ln)
+            k ^= 1
 
     def close(self):
-        self.host.free()
-        self.h_len.free()
+        for s in self._sets:
+            s.close()
 
 
 class TxPipeline:
@@ -64,54 +134,116 @@ class TxPipeline:
     -> one H2D copy -> rns_tx_fill_dev (IPv4 header + L4 checksums, pseudo-headers on the
     device) -> D2H of each slot's first HEAD bytes (every byte the fill can change)
     -> rns_io_send_batch (one writev per datagram, like tun_send via send_packet,
-    netif.rs:85-98)."""
+    netif.rs:85-98).
+
+    ``send`` does one batch synchronously.  ``submit`` / ``complete`` overlap: submit
+    queues a batch's GPU work and returns; complete waits for the oldest submitted
+    batch and writes it to the fd.  With two buffer sets, the caller fills the next
+    batch's ``slots()`` and the host sends one batch while the GPU finalizes the other:
+
+        for lengths in batches:
+            if pipe.pending() == pipe.DEPTH:
+                statuses.append(pipe.complete(fd))
+            fill(pipe.slots(), ...)
+            pipe.submit(lengths)
+        while pipe.pending():
+            statuses.append(pipe.complete(fd))
+    """
 
     HEAD = 128  # the fill writes only below byte 96 of a slot-aligned datagram
+    DEPTH = 2
 
     def __init__(self, device: int = 0, max_pkts: int = 65536, slot_bytes: int = MRU):
         self.slot = slot_bytes
         self.max_pkts = max_pkts
         self.dev = torch.device(f"cuda:{device}")
-        self.host = PinnedBuffer(slot_bytes * max_pkts)
-        self.h_len = PinnedBuffer(4 * max_pkts)
-        self.h_head = PinnedBuffer(self.HEAD * max_pkts)
-        self.d_arena = torch.empty(slot_bytes * max_pkts, dtype=torch.uint8, device=self.dev)
+        self._sets = [_Slots(self.dev, max_pkts, slot_bytes, head=self.HEAD) for _ in range(self.DEPTH)]
         self.d_off = (torch.arange(max_pkts, dtype=torch.int64, device=self.dev) * slot_bytes).contiguous()
         self.off = np.arange(max_pkts, dtype=np.uint64) * np.uint64(slot_bytes)
-        self.d_len = torch.empty(max_pkts, dtype=torch.int32, device=self.dev)
-        self.d_status = torch.empty(max_pkts, dtype=torch.uint8, device=self.dev)
+        self._next = 0                    # the set slots() hands out
+        self._inflight: deque = deque()   # (set, lengths), oldest first
+        self._stream = None
 
     def slots(self) -> np.ndarray:
-        """The pinned slots, shape (max_pkts, slot_bytes): datagram i goes in row i."""
-        return self.host.array[: self.slot * self.max_pkts].reshape(self.max_pkts, self.slot)
+        """The free set's pinned slots, shape (max_pkts, slot_bytes): datagram i goes in row i."""
+        if len(self._inflight) == self.DEPTH:
+            raise RuntimeError("every buffer set is in flight: complete() one first")
+        return self._sets[self._next].host.array[: self.slot * self.max_pkts].reshape(self.max_pkts, self.slot)
 
-    def send(self, fd: int, lengths: np.ndarray) -> np.ndarray:
-        """Fill and send the datagrams in slots [0, n); returns their RNS_TX_* status."""
+    def pending(self) -> int:
+        return len(self._inflight)
+
+    def _check(self, lengths: np.ndarray) -> np.ndarray:
         n = int(lengths.shape[0])
-        if n == 0:
-            return np.empty(0, dtype=np.uint8)
         if n > self.max_pkts:
             raise ValueError("more datagrams than slots")
         ln = np.ascontiguousarray(lengths, dtype=np.uint32)
-        if int(ln.max()) > self.slot:
+        if n and int(ln.max()) > self.slot:
             raise ValueError("datagram longer than its slot")
-        hl = self.h_len.array.view(np.uint32)[:n]
+        return ln
+
+    def _queue(self, s: _Slots, ln: np.ndarray) -> None:
+        n = ln.shape[0]
+        hl = s.h_len.array.view(np.uint32)[:n]
         hl[:] = ln
-        head = self.h_head.array[: self.HEAD * n].reshape(n, self.HEAD)
-        with torch.cuda.device(self.dev):
-            self.d_arena[: n * self.slot].copy_(torch.from_numpy(self.host.array[: n * self.slot]), non_blocking=True)
-            self.d_len[:n].copy_(torch.from_numpy(hl.view(np.int32)), non_blocking=True)
-            tx_fill(self.d_arena, self.d_off[:n], self.d_len[:n], status=self.d_status[:n])
-            heads = self.d_arena[: n * self.slot].view(n, self.slot)[:, : self.HEAD].contiguous()
-            torch.from_numpy(head).copy_(heads, non_blocking=True)
-            status = self.d_status[:n].cpu().numpy()   # synchronises: the heads have landed too
-        self.slots()[:n, : self.HEAD] = head
-        sent = send_batch(fd, self.host.array, self.off[:n], ln)
+        head = s.h_head.array[: self.HEAD * n].reshape(n, self.HEAD)
+        s.d_arena[: n * self.slot].copy_(torch.from_numpy(s.host.array[: n * self.slot]), non_blocking=True)
+        s.d_len[:n].copy_(torch.from_numpy(hl.view(np.int32)), non_blocking=True)
+        tx_fill(s.d_arena, self.d_off[:n], s.d_len[:n], status=s.d_status[:n])
+        heads = s.d_arena[: n * self.slot].view(n, self.slot)[:, : self.HEAD].contiguous()
+        torch.from_numpy(head).copy_(heads, non_blocking=True)
+        torch.from_numpy(s.h_status.array[:n]).copy_(s.d_status[:n], non_blocking=True)
+        s.done.record()
+
+    def _finish(self, fd: int, s: _Slots, ln: np.ndarray) -> np.ndarray:
+        n = ln.shape[0]
+        s.done.synchronize()
+        slots = s.host.array[: self.slot * n].reshape(n, self.slot)
+        slots[:, : self.HEAD] = s.h_head.array[: self.HEAD * n].reshape(n, self.HEAD)
+        sent = send_batch(fd, s.host.array, self.off[:n], ln)
         if sent != n:
             raise OSError(f"sent {sent} of {n} datagrams")
-        return status
+        return s.h_status.array[:n].copy()
+
+    def send(self, fd: int, lengths: np.ndarray) -> np.ndarray:
+        """Fill and send the datagrams in slots [0, n) of ``slots()``; returns their
+        RNS_TX_* status."""
+        if self._inflight:
+            raise RuntimeError("submitted batches pending: complete() them first")
+        ln = self._check(lengths)
+        if ln.shape[0] == 0:
+            return np.empty(0, dtype=np.uint8)
+        s = self._sets[self._next]
+        with torch.cuda.device(self.dev):
+            self._queue(s, ln)
+        return self._finish(fd, s, ln)
+
+    def submit(self, lengths: np.ndarray) -> None:
+        """Queue the GPU work for slots [0, n) of ``slots()`` and hand out the other set."""
+        if len(self._inflight) == self.DEPTH:
+            raise RuntimeError("every buffer set is in flight: complete() one first")
+        ln = self._check(lengths)
+        s = self._sets[self._next]
+        with torch.cuda.device(self.dev):
+            if self._stream is None:
+                self._stream = torch.cuda.Stream(self.dev)
+            with torch.cuda.stream(self._stream):
+                if ln.shape[0]:
+                    self._queue(s, ln)
+                else:
+                    s.done.record()
+        self._inflight.append((s, ln))
+        self._next = (self._next + 1) % self.DEPTH
+
+    def complete(self, fd: int) -> np.ndarray:
+        """Wait for the oldest submitted batch, send it; returns its RNS_TX_* status."""
+        if not self._inflight:
+            raise RuntimeError("nothing submitted")
+        s, ln = self._inflight.popleft()
+        if ln.shape[0] == 0:
+            return np.empty(0, dtype=np.uint8)
+        return self._finish(fd, s, ln)
 
     def close(self):
-        self.host.free()
-        self.h_len.free()
-        self.h_head.free()
+        for s in self._sets:
+            s.close()

@@ -82,3 +82,84 @@ def test_tx_pipeline_to_socket(oracle):
     assert len(received) == len(pkts)
     bad = [i for i in range(len(pkts)) if received[i] != want[i][0]]
     assert not bad, bad[:5]
+
+
+def test_stream_overlapped(oracle):
+    """RxPipeline.stream: the host reads batch k+1 while batch k is verified; verdicts,
+    lengths and slot bytes as the synchronous path would give them."""
+    pkts = [p for p in make_packets(6000, 0x0BE1) if len(p) > 0]
+    lens = np.array([len(p) for p in pkts], dtype=np.uint32)
+    off = np.zeros(len(pkts), dtype=np.uint64)
+    np.cumsum(lens[:-1].astype(np.uint64), out=off[1:])
+    arena = np.frombuffer(b"".join(pkts), dtype=np.uint8).copy()
+    expect = np.array([O.rx_status_ref(p, L4, L6, ones_comp=oracle.compute_ones_comp) for p in pkts], dtype=np.uint8)
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+    t = threading.Thread(target=send_batch, args=(a.fileno(), arena, off, lens))
+    t.start()
+    pipe = RxPipeline(L4, L6, device=0, max_pkts=512)
+    got_st, got_len, bad_bytes, i = [], [], 0, 0
+    for st, ln, slots in pipe.stream(b.fileno(), timeout_ms=2000):
+        got_st.append(st.copy())
+        got_len.append(ln.copy())
+        for k in range(ln.shape[0]):
+            bad_bytes += slots[k, : ln[k]].tobytes() != pkts[i + k]
+        i += ln.shape[0]
+        if i >= len(pkts):
+            break
+    t.join()
+    pipe.close()
+    a.close()
+    b.close()
+    assert len(got_st) >= 2 and bad_bytes == 0
+    assert np.array_equal(np.concatenate(got_len), lens)
+    assert np.array_equal(np.concatenate(got_st), expect)
+
+
+def test_tx_overlapped_to_socket(oracle):
+    """TxPipeline.submit/complete: two buffer sets in flight; the far end receives
+    exactly what the reference's transmit path would send, in order."""
+    from rustnetworkstack_amd.batch import recv_batch
+    from rustnetworkstack_amd.pipeline import TxPipeline
+    from test_gpu_tx import outgoing
+    pkts = [p for p in outgoing(5000, 0x7A11) if 0 < len(p) <= 2048]
+    want = [O.tx_fill_ref(p, ones_comp=oracle.compute_ones_comp) for p in pkts]
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+    for s_, opt in ((a, socket.SO_SNDBUF), (b, socket.SO_RCVBUF)):
+        s_.setsockopt(socket.SOL_SOCKET, opt, 32 << 20)
+    received = []
+
+    def drain():
+        buf = np.empty(2048 * 1024, dtype=np.uint8)
+        while len(received) < len(pkts):
+            off, ln = recv_batch(b.fileno(), buf, 2048, 1024, timeout_ms=5000)
+            if ln.shape[0] == 0:
+                return
+            received.extend(buf[int(o):int(o) + int(n)].tobytes() for o, n in zip(off, ln))
+
+    t = threading.Thread(target=drain)
+    t.start()
+    pipe = TxPipeline(device=0, max_pkts=700)
+    statuses = []
+    with pytest.raises(RuntimeError):
+        pipe.complete(a.fileno())
+    for i0 in range(0, len(pkts), 700):
+        if pipe.pending() == pipe.DEPTH:
+            statuses.append(pipe.complete(a.fileno()))
+        chunk = pkts[i0:i0 + 700]
+        slots = pipe.slots()
+        for k, p in enumerate(chunk):
+            slots[k, :len(p)] = np.frombuffer(p, dtype=np.uint8)
+        pipe.submit(np.array([len(p) for p in chunk], dtype=np.uint32))
+        if pipe.pending() == pipe.DEPTH:
+            with pytest.raises(RuntimeError):
+                pipe.slots()
+    while pipe.pending():
+        statuses.append(pipe.complete(a.fileno()))
+    t.join(timeout=60)
+    pipe.close()
+    a.close()
+    b.close()
+    assert np.array_equal(np.concatenate(statuses), np.array([w[1] for w in want], dtype=np.uint8))
+    assert len(received) == len(pkts)
+    bad = [i for i in range(len(pkts)) if received[i] != want[i][0]]
+    assert not bad, bad[:5]

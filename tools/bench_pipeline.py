@@ -8,7 +8,11 @@ Transmit (--tx): the same datagrams with their checksum fields zeroed are placed
 TxPipeline's pinned slots and sent (H2D -> rns_tx_fill_dev -> header bytes D2H ->
 rns_io_send_batch); a drain thread reads them and the result is spot-checked.
 
-    python tools/bench_pipeline.py [--packets 262144] [--batch 8192] [--tx]
+    python tools/bench_pipeline.py [--packets 262144] [--batch 8192] [--tx] [--overlap]
+
+--overlap runs the two-buffer-set forms (RxPipeline.stream, TxPipeline.submit/complete):
+the GPU work of one batch is queued on its own stream while the host reads or writes
+the datagrams of the other.
 """
 import argparse
 import json
@@ -36,6 +40,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--out", default="")
     ap.add_argument("--tx", action="store_true")
+    ap.add_argument("--overlap", action="store_true")
     args = ap.parse_args()
     if args.tx:
         return main_tx(args)
@@ -53,6 +58,13 @@ def main():
     t0 = time.perf_counter()
     sender.start()
     got = accepted = batches = 0
+    if args.overlap:
+        for st, ln, _ in pipe.stream(r.fileno(), timeout_ms=5000):
+            got += st.shape[0]
+            accepted += int((st == 0x43).sum())
+            batches += 1
+            if got >= lay.n:
+                break
     while got < lay.n:
         st, ln = pipe.receive(r.fileno(), timeout_ms=5000)
         if st.shape[0] == 0:
@@ -64,6 +76,7 @@ def main():
     sender.join()
     res = {"packets": lay.n, "received": got, "accepted": accepted, "batches": batches,
            "seconds": round(dt, 3), "packets_per_s": round(got / dt), "GBps": round(got * 1500 / dt / 1e9, 3),
+           "overlap": args.overlap,
            "path": "AF_UNIX SOCK_SEQPACKET socketpair (TUN-like) -> rns_io_recv_batch (2048-B slots, pinned) -> "
                    "H2D -> rns_rx_verify_dev -> status D2H; sender on another host thread"}
     print(json.dumps(res))
@@ -108,13 +121,19 @@ def main_tx(args):
     filled = 0
     for i0 in range(0, n, args.batch):
         k = min(args.batch, n - i0)
+        if args.overlap and pipe.pending() == pipe.DEPTH:
+            filled += int((pipe.complete(a.fileno()) == 3).sum())
         pipe.slots()[:k, :1500] = unfilled[i0:i0 + k]
-        st = pipe.send(a.fileno(), np.full(k, 1500, dtype=np.uint32))
-        filled += int((st == 3).sum())
+        if args.overlap:
+            pipe.submit(np.full(k, 1500, dtype=np.uint32))
+        else:
+            filled += int((pipe.send(a.fileno(), np.full(k, 1500, dtype=np.uint32)) == 3).sum())
+    while pipe.pending():
+        filled += int((pipe.complete(a.fileno()) == 3).sum())
     t.join()
     dt = time.perf_counter() - t0
     exact = all(np.array_equal(v, dgrams[i]) for i, v in sample.items())
-    res = {"direction": "transmit", "packets": n, "received": got[0], "filled": filled,
+    res = {"direction": "transmit", "overlap": args.overlap, "packets": n, "received": got[0], "filled": filled,
            "sample_exact": exact, "sampled": len(sample), "seconds": round(dt, 3),
            "packets_per_s": round(got[0] / dt), "GBps": round(got[0] * 1500 / dt / 1e9, 3),
            "path": "host datagrams -> pinned 2048-B slots -> H2D -> rns_tx_fill_dev -> 128 B/slot D2H -> "
