@@ -160,7 +160,7 @@ __global__ __launch_bounds__(kBlock) void csum_batch_kernel(const CsumArgs a)
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const uint32_t c = c0 + u * G;
-                    if (c == 0 || c == last) {
+                    if ((c == 0 && s != 0) || (c == last && e != 16)) {
                         const int lo = (c == 0) ? static_cast<int>(s) : 0;
                         const int hi = (c == last) ? e : 16;
                         v[u].x = keep_bytes(v[u].x, lo, hi, 0);
@@ -381,7 +381,9 @@ __device__ __forceinline__ void mask_edges(const Pkt &k, uint32_t c0, uint4 (&v)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t c = c0 + u * G;
-        if (c == 0 || c + 1 == k.nch) {
+        // (a chunk-aligned start or end needs no mask: with 16-byte-aligned packet
+        // starts the head chunk is skipped by the whole wave)
+        if ((c == 0 && k.s != 0) || (c + 1 == k.nch && k.e != 16)) {
             const int lo = (c == 0) ? k.s : 0;
             const int hi = (c + 1 == k.nch) ? k.e : 16;
             v[u].x = keep_bytes(v[u].x, lo, hi, 0);
