@@ -9,7 +9,15 @@ CSRC     := $(PKG)/csrc
 BUILD    := $(PKG)/build
 LIB      := $(PKG)/librns_checksum.so
 
-all: $(LIB) oracle
+CABI_TEST := tests/c/test_batch_abi
+
+all: $(LIB) oracle $(CABI_TEST)
+
+# A plain C caller of the C ABI (no torch): built here, run by tests/test_c_caller.py on a GPU.
+$(CABI_TEST): tests/c/test_batch_abi.c oracle/csum_oracle.c include/rns_checksum.h $(LIB)
+	gcc -std=gnu11 -O1 -Wall -Wextra -Werror -D__HIP_PLATFORM_AMD__ -Iinclude -I/opt/rocm/include \
+	    tests/c/test_batch_abi.c oracle/csum_oracle.c -L$(PKG) -lrns_checksum -Wl,-rpath,'$$ORIGIN/../../$(PKG)' \
+	    -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib -lpthread -o $@
 
 $(BUILD)/rns_checksum.o: $(CSRC)/rns_checksum.hip include/rns_checksum.h
 	@mkdir -p $(BUILD)
@@ -51,7 +59,7 @@ asm: $(CSRC)/rns_checksum.hip
 	cd $(BUILD)/asm && $(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -I../../../include -c ../../../$< -o rns.o -save-temps
 
 clean:
-	rm -rf $(BUILD) $(LIB)
+	rm -rf $(BUILD) $(LIB) $(CABI_TEST)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle resources asm clean ab
