@@ -33,8 +33,11 @@ def test_c_caller_builds_and_fails_loudly_without_gpu(tmp_path):
 
 
 @pytest.mark.gpu
-def test_c_caller_on_gpu():
-    assert os.path.exists(EXE), "build first: make (builds tests/c/test_batch_abi)"
-    r = subprocess.run([EXE], capture_output=True, text=True, timeout=120)
+def test_c_caller_on_gpu(tmp_path):
+    exe = EXE
+    if not os.path.exists(exe):  # `make` builds it in-tree; a tree without it gets a private copy
+        exe = str(tmp_path / "test_batch_abi")
+        _compile(exe)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "all checks passed" in r.stdout
