@@ -10,6 +10,7 @@
 //   read                 one wave per 64 packets streams their bytes (16 B/lane, 4 in flight)
 //   read+store{2,32}     the same, then each lane stores into one packet's field
 //   read+compact         the same, then one coalesced 128-B store of 64 u16 results
+//   glds{4,8,16}         the slab through an LDS ring with global_load_lds (DEPTH-1 KB blocks in flight)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -125,6 +126,50 @@ __global__ __launch_bounds__(256) void read_store(uint8_t *arena, uint32_t n, ui
     }
 }
 
+// LDS-DMA streaming: each wave streams its slab in 1 KB blocks with global_load_lds
+// (16 B per lane, no VGPR destination) into a DEPTH-block LDS ring, DEPTH-1 blocks in
+// flight, one counted vmcnt wait per block, then ds_read_b128 + v_sad_u16.
+template <int DEPTH>
+__global__ __launch_bounds__(256) void read_glds(const uint8_t *arena, uint32_t n, uint32_t stride, uint16_t *out)
+{
+    extern __shared__ uint4 ring[];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
+    const uint64_t p0 = static_cast<uint64_t>(wave) * 64;
+    if (p0 >= n)
+        return;
+    const uint32_t np = min(64u, n - static_cast<uint32_t>(p0));
+    const uint8_t *base = arena + p0 * stride;
+    const uint32_t nblk = static_cast<uint32_t>((static_cast<uint64_t>(np) * stride) >> 10);
+    typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+    lds_u32x4 *myring = (lds_u32x4 *)(ring + wv * DEPTH * 64);  // addrspacecast: ds_read, not flat
+    auto issue = [&](uint32_t blk) {  // past the end: re-read the last block (keeps the count constant)
+        const uint32_t b = blk < nblk ? blk : nblk - 1;
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(base + static_cast<uint64_t>(b) * 1024 + lane * 16),
+                                         (__attribute__((address_space(3))) void *)(myring + (blk % DEPTH) * 64),
+                                         16, 0, 2);
+    };
+#pragma unroll
+    for (int d = 0; d < DEPTH - 1; ++d)
+        issue(d);
+    uint32_t acc = 0;
+    for (uint32_t b = 0; b < nblk; ++b) {
+        issue(b + DEPTH - 1);
+        // vmcnt(DEPTH-1): block b has landed (gfx9 encoding: vmcnt[3:0], expcnt 7, lgkmcnt 15)
+        __builtin_amdgcn_s_waitcnt((DEPTH - 1) | 0xF70);
+        __asm__ volatile("" ::: "memory");
+        const u32x4 x = *(volatile lds_u32x4 *)(myring + (b % DEPTH) * 64 + lane);
+        acc = __builtin_amdgcn_sad_u16(x.x, 0, acc);
+        acc = __builtin_amdgcn_sad_u16(x.y, 0, acc);
+        acc = __builtin_amdgcn_sad_u16(x.z, 0, acc);
+        acc = __builtin_amdgcn_sad_u16(x.w, 0, acc);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the read is done before the slot is refilled
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // drain the DMA before the wave ends
+    if (acc == 0x12345678u)
+        out[p0 + lane] = 1;
+}
+
 template <class F>
 static float time_ms(F launch, int iters)
 {
@@ -188,6 +233,10 @@ int main(int argc, char **argv)
         report("read_plain+store32", time_ms([&] { read_store<2, 0><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
         report("read_plain+inline16", time_ms([&] { read_store<4, 0><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
         report("read_plain+deferred16", time_ms([&] { read_store<5, 0><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("glds4", time_ms([&] { read_glds<4><<<rblocks, 256, 4 * 4 * 1024>>>(arena, n, stride, out); }, iters));
+        report("glds8", time_ms([&] { read_glds<8><<<rblocks, 256, 4 * 8 * 1024>>>(arena, n, stride, out); }, iters));
+        report("glds8_occ2", time_ms([&] { read_glds<8><<<rblocks, 256, 80 << 10>>>(arena, n, stride, out); }, iters));
+        report("glds16", time_ms([&] { read_glds<16><<<rblocks, 256, 4 * 16 * 1024>>>(arena, n, stride, out); }, iters));
         report("read;scatter32", time_ms([&] {
                    read_store<3><<<rblocks, 256>>>(arena, n, stride, out);
                    scatter<32><<<sblocks, 256>>>(arena, n, stride, 7);
