@@ -8,6 +8,7 @@
 * concurrent callers: host batches from several threads (one staging context each,
   the threading model of SURVEY §8b) and device batches on several streams.
 """
+import os
 import threading
 
 import numpy as np
@@ -60,7 +61,11 @@ def expected(oracle, arena_np, off, ln, sd, bad, complement):
     return exp
 
 
-@pytest.mark.parametrize("seed", [1, 2, 3])
+# RNS_FUZZ_SEEDS="4,5,..." runs a longer campaign with the same tests
+SEEDS = [int(x) for x in os.environ.get("RNS_FUZZ_SEEDS", "1,2,3").split(",") if x]
+
+
+@pytest.mark.parametrize("seed", SEEDS)
 def test_random_descriptors_every_kernel(oracle, seed):
     arena_np = O.splitmix64_bytes(0xF0 + seed, ARENA)
     arena = torch.from_numpy(arena_np).to(DEV)
@@ -80,9 +85,10 @@ def test_random_descriptors_every_kernel(oracle, seed):
             assert int(cnt.item()) == int(bad.sum()), (shape, hint)
 
 
-def test_garbage_datagrams_match_reference_receive_path(oracle):
+@pytest.mark.parametrize("seed", SEEDS[:1] if "RNS_FUZZ_SEEDS" not in os.environ else SEEDS)
+def test_garbage_datagrams_match_reference_receive_path(oracle, seed):
     n = 6000
-    w = O.splitmix64_words(0x6A4B, 2 * n)
+    w = O.splitmix64_words(0x6A4B + seed - 1, 2 * n)
     pkts = []
     for i in range(n):
         L = int(w[2 * i] % np.uint64(3000))
