@@ -2009,8 +2009,9 @@ const char *rns_csum_shape_name(uint32_t len_hint)
 
 const char *rns_build_info(void)
 {
-    return "rns_checksum abi=1 offload-arch=gfx950 kernels=csum_rounds_kernel/csum_batch_kernel<G,U,NT> "
-           "(dot4 BE-half sums, wave64, DPP group reduction)";
+    return "rns_checksum abi=1 offload-arch=gfx950 kernels=csum_mixed_kernel (per-wave size-class sort; "
+           "verify / fill / transmit-finalize stash modes), csum_rounds_kernel, csum_batch_kernel, "
+           "chain_combine_kernel (v_sad_u16 LE sums, v_dot4 BE sums past 128 KiB, wave64, DPP reductions)";
 }
 
 int rns_device_count(void)
