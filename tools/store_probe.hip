@@ -10,6 +10,7 @@
 //   read                 one wave per 64 packets streams their bytes (16 B/lane, 4 in flight)
 //   read+store{2,32}     the same, then each lane stores into one packet's field
 //   read+compact         the same, then one coalesced 128-B store of 64 u16 results
+//   read_xcd             read, with blocks renumbered so each XCD streams a contiguous eighth
 //   glds{4,8,16}         the slab through an LDS ring with global_load_lds (DEPTH-1 KB blocks in flight)
 #include <hip/hip_runtime.h>
 
@@ -44,16 +45,25 @@ __global__ __launch_bounds__(256) void scatter(uint8_t *arena, uint32_t n, uint3
     }
 }
 
+// XCD-contiguous block order: dispatch sends block b to XCD b % 8, so block b takes
+// slab (b % 8) * (nblk / 8) + b / 8 and each XCD streams one contiguous eighth.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nblk)
+{
+    const uint32_t per = nblk / 8;
+    return (b < per * 8) ? (b % 8) * per + b / 8 : b;
+}
+
 // MODE 0: read only; 1: + 2-byte field store; 2: + 32-byte sector store; 3: + compact u16 store
 // at the end of the wave's slab.  MODE 4: the lane that loaded a packet's field chunk
 // rewrites that 16-B chunk right after consuming it; MODE 5: the same store issued one
 // iteration later, after the next iteration's loads (so no load waits for it).
 // CACHE: buffer-load cache policy bits (0 = default, 2 = nontemporal).
-template <int MODE, int CACHE = 2>
+template <int MODE, int CACHE = 2, bool XCD = false>
 __global__ __launch_bounds__(256) void read_store(uint8_t *arena, uint32_t n, uint32_t stride, uint16_t *out)
 {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
+    const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t wave = (blk * 256 + threadIdx.x) >> 6;
     const uint64_t p0 = static_cast<uint64_t>(wave) * 64;
     if (p0 >= n)
         return;
@@ -233,6 +243,8 @@ int main(int argc, char **argv)
         report("read_plain+store32", time_ms([&] { read_store<2, 0><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
         report("read_plain+inline16", time_ms([&] { read_store<4, 0><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
         report("read_plain+deferred16", time_ms([&] { read_store<5, 0><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read_xcd", time_ms([&] { read_store<0, 2, true><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read_xcd_occ2", time_ms([&] { read_store<0, 2, true><<<rblocks, 256, 80 << 10>>>(arena, n, stride, out); }, iters));
         report("glds4", time_ms([&] { read_glds<4><<<rblocks, 256, 4 * 4 * 1024>>>(arena, n, stride, out); }, iters));
         report("glds8", time_ms([&] { read_glds<8><<<rblocks, 256, 4 * 8 * 1024>>>(arena, n, stride, out); }, iters));
         report("glds8_occ2", time_ms([&] { read_glds<8><<<rblocks, 256, 80 << 10>>>(arena, n, stride, out); }, iters));
