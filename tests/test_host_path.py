@@ -1,6 +1,5 @@
 """The product's per-packet host entry points (rns_compute_*, via the util.rs
 mirror rustnetworkstack_amd.util) against the reference KATs and the oracle."""
-import numpy as np
 import pytest
 
 from conftest import expand_fragment, sweep_arena
