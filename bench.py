@@ -36,6 +36,9 @@ def parse_args(argv=None):
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="c3_1500B")
+    p.add_argument("--desc", choices=("auto", "64", "32"), default="auto",
+                   help="descriptor offset width: 32 = compact form (rns_csum_batch_dev_off32); "
+                        "auto = 32 when the arena is below 4 GiB")
     p.add_argument("--shape", default="", help="variant,G,U,max_blocks kernel shape override (tuning)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample duration (single thread)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -130,7 +133,7 @@ def timed_loop(engine, dist: Dist, steps: int, warmup: int) -> dict:
 # ---------------------------------------------------------------------------
 class GpuEngine:
     def __init__(self, config: str, rank: int, local_rank: int, shape=None, gather_dist: Dist | None = None,
-                 steps: int = 0, world: int = 1, strong: bool = False):
+                 steps: int = 0, world: int = 1, strong: bool = False, compact="64"):
         import torch
 
         from rustnetworkstack_amd.workloads import DATA_SEED, DeviceBatch, make_layout
@@ -152,6 +155,11 @@ class GpuEngine:
         nrot = max(1, -(-(768 << 20) // max(self.layout.arena_bytes, 1))) if small else 1
         self.batches = [DeviceBatch(self.layout if r == 0 else layout(r), self.device) for r in range(nrot)]
         self.shape = shape
+        if compact == "auto":
+            compact = shape is None and self.layout.arena_bytes + 16 < 2 ** 32
+        self.compact = compact in (True, "32")
+        for b in self.batches:  # bind every rotating batch (and upload compact offsets) before any timing
+            b.launcher(complement=True, shape=shape, compact=self.compact)
         self.gather = gather_dist
         self.k = 0
         self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -172,7 +180,7 @@ class GpuEngine:
     def step(self):
         b = self.batches[self.k % len(self.batches)]
         self.k += 1
-        b.launcher(complement=True, shape=self.shape)()  # pre-bound: one ctypes call
+        b.launcher(complement=True, shape=self.shape, compact=self.compact)()  # pre-bound: one ctypes call
         if self.gather is not None and self.gather.enabled:
             self.gather.dist.all_gather_into_tensor(self.gathered, b.out.view(self.torch.int16))
 
@@ -292,7 +300,8 @@ def main(argv=None):
     shape = tuple(int(x) for x in args.shape.split(",")) if args.shape else None
     strong = args.scaling == "strong" or (args.scaling == "auto" and args.config == "c5_imix")
     engine = GpuEngine(args.config, dist.rank, dist.local_rank, shape=shape,
-                       gather_dist=dist if args.gather else None, steps=args.steps, world=dist.world, strong=strong)
+                       gather_dist=dist if args.gather else None, steps=args.steps, world=dist.world, strong=strong,
+                       compact=args.desc)
     r = timed_loop(engine, dist, args.steps, args.warmup)
     elapsed = r["elapsed_s"]
     # all ranks' payload (strong: the shards add up to the config's one batch)
@@ -324,6 +333,8 @@ def main(argv=None):
             "parallelism": f"packet shards x{dist.world}, no data-path collective"
                            + (" + RCCL all_gather of results" if args.gather else ""),
             "kernel_shape": list(shape) if shape else "auto",
+            "descriptors": ("u32 offset + u32 length + u16 seed (rns_csum_batch_dev_off32)" if engine.compact
+                            else "u64 offset + u32 length + u16 seed (rns_csum_batch_dev)"),
             "rotating_batches": len(engine.batches),
         },
         "roofline": {

@@ -49,6 +49,10 @@ class PreparedBatch:
 
     ``shape`` = (variant, lanes_per_packet, unroll, max_blocks) overrides the
     automatic kernel shape (tuning); see rns_csum_batch_dev_cfg.
+
+    ``off`` is int64, or int32 for the compact descriptor form
+    (rns_csum_batch_dev_off32: the tensor holds unsigned 32-bit offsets, arenas
+    below 4 GiB; 10 B of descriptors per packet instead of 14).
     """
 
     def __init__(self, arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor,
@@ -56,8 +60,11 @@ class PreparedBatch:
                  len_hint: int = 0, bad: torch.Tensor | None = None,
                  shape: tuple[int, int, int, int] | None = None):
         _require_cuda(arena, "arena", (torch.uint8,))
-        _require_cuda(off, "off", (torch.int64,))
+        _require_cuda(off, "off", (torch.int64, torch.int32))
         _require_cuda(length, "length", (torch.int32,))
+        compact = off.dtype == torch.int32
+        if compact and shape is not None:
+            raise ValueError("shape overrides take 64-bit offsets")
         n = off.numel()
         if length.numel() != n:
             raise ValueError("off and length must have the same number of packets")
@@ -91,8 +98,9 @@ class PreparedBatch:
         self.out = out
         self.n = n
         self.device = dev
+        self._name = "rns_csum_batch_dev_off32" if compact else "rns_csum_batch_dev"
         if shape is None:
-            self._fn = lib.rns_csum_batch_dev
+            self._fn = getattr(lib, self._name)
             self._args = (arena.data_ptr(), arena.numel(), off.data_ptr(), length.data_ptr(), seed_ptr,
                           out.data_ptr(), n, flags, int(len_hint), bad_ptr, stream)
         else:
@@ -111,7 +119,7 @@ class PreparedBatch:
             else:
                 st = self._fn(*self._args)
             if st != _lib.RNS_OK:
-                raise _lib.ChecksumError(st, "rns_csum_batch_dev")
+                raise _lib.ChecksumError(st, self._name)
         return self.out
 
 

@@ -49,6 +49,7 @@ struct CsumArgs {
     uint64_t arena_bytes;      // valid bytes from `arena` (after base_adjust)
     uint64_t base_adjust;      // added to every packet offset (caller base was not 16-aligned)
     const uint64_t *off;       // per-packet byte offsets (null in strided mode)
+    const uint32_t *off32;     // compact form: 32-bit offsets for arenas < 4 GiB (used when non-null)
     const uint32_t *len;       // per-packet lengths (null in strided mode)
     const uint16_t *seed;      // per-packet seeds, null => 0
     uint16_t *out;
@@ -67,6 +68,14 @@ struct CsumArgs {
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Descriptor offset of packet p: the compact 32-bit form when the caller passed one
+// (10 B of descriptors per packet instead of 14), else the 64-bit form.  The branch
+// is on a kernel argument, so it is uniform.
+__device__ __forceinline__ uint64_t desc_off(const CsumArgs &a, uint64_t p)
+{
+    return a.off32 ? static_cast<uint64_t>(a.off32[p]) : a.off[p];
+}
 
 // Cache-policy bits of the "nontemporal" buffer loads (gfx950 CPol: 1 = sc0, 2 = nt,
 // 16 = sc1).  A/B knob: -DRNS_NT_AUX=...
@@ -129,7 +138,7 @@ __global__ __launch_bounds__(kBlock) void csum_batch_kernel(const CsumArgs a)
             start = a.first_off + static_cast<uint64_t>(p) * a.stride;
             L = a.fixed_len;
         } else {
-            start = a.off[p];
+            start = desc_off(a, p);
             L = a.len[p];
         }
         start += a.base_adjust;
@@ -535,7 +544,7 @@ __global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
                 d_start = a.first_off + p * a.stride;
                 d_len = a.fixed_len;
             } else {
-                d_start = a.off[p];
+                d_start = desc_off(a, p);
                 d_len = a.len[p];
             }
             d_seed = a.seed ? a.seed[p] : 0u;
@@ -909,7 +918,7 @@ __device__ __forceinline__ Desc<BUF> load_desc(const CsumArgs &a, uint64_t p)
         off = a.first_off + q * a.stride;
         d.len = a.fixed_len;
     } else {
-        off = a.off[q];
+        off = desc_off(a, q);
         d.len = a.len[q];
     }
     if constexpr (BUF)
@@ -1541,6 +1550,29 @@ int rns_csum_batch_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
     const Shape sh = pick_shape(len_hint);
     return rns_csum_batch_dev_cfg(d_arena, arena_bytes, d_off, d_len, d_seed, d_out, n, flags, sh.variant, sh.G,
                                   sh.U, sh.max_blocks, d_bad, stream);
+}
+
+int rns_csum_batch_dev_off32(const uint8_t *d_arena, uint64_t arena_bytes, const uint32_t *d_off32,
+                             const uint32_t *d_len, const uint16_t *d_seed, uint16_t *d_out, uint32_t n,
+                             uint32_t flags, uint32_t len_hint, uint32_t *d_bad, void *stream)
+{
+    if (n == 0)
+        return RNS_OK;
+    if (!d_arena || !d_off32 || !d_len || !d_out)
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    const Shape sh = pick_shape(len_hint);
+    CsumArgs a{};
+    set_arena(a, d_arena, arena_bytes);
+    a.off32 = d_off32;
+    a.len = d_len;
+    a.seed = d_seed;
+    a.out = d_out;
+    a.bad = d_bad;
+    a.n = n;
+    a.flags = flags;
+    return dispatch<false>(a, sh.variant, sh.G, sh.U, sh.max_blocks, static_cast<hipStream_t>(stream));
 }
 
 int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uint64_t first_off,

@@ -130,12 +130,20 @@ class DeviceBatch:
         self.out = torch.empty(layout.n, dtype=torch.uint16, device=self.device)
         self._prepared = {}
 
-    def launcher(self, complement: bool = False, shape=None):
-        """Pre-bound launch (one ctypes call per launch) on the current stream."""
+    def launcher(self, complement: bool = False, shape=None, compact: bool = False):
+        """Pre-bound launch (one ctypes call per launch) on the current stream.
+        ``compact`` binds 32-bit offsets (rns_csum_batch_dev_off32; arenas < 4 GiB)."""
+        import torch
+
         from .batch import PreparedBatch
-        key = (complement, shape)
+        key = (complement, shape, compact)
         if key not in self._prepared:
-            self._prepared[key] = PreparedBatch(self.arena, self.off, self.length, self.seed, complement=complement,
+            off = self.off
+            if compact:
+                if self.layout.arena_bytes + 16 >= 2 ** 32:
+                    raise ValueError("compact descriptors need an arena below 4 GiB")
+                off = torch.from_numpy(self.layout.off.astype(np.uint32).view(np.int32)).to(self.device)
+            self._prepared[key] = PreparedBatch(self.arena, off, self.length, self.seed, complement=complement,
                                                 out=self.out, len_hint=int(round(self.layout.mean_len)), shape=shape)
         return self._prepared[key]
 

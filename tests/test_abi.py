@@ -57,6 +57,8 @@ def test_batch_calls_fail_loudly_without_gpu():
     fake = ctypes.c_void_p(4096)
     st = lib.rns_csum_batch_dev(fake, 16, fake, fake, None, ctypes.addressof(out), 1, 0, 0, None, None)
     assert st == _lib.RNS_E_NODEVICE
+    st = lib.rns_csum_batch_dev_off32(fake, 16, fake, fake, None, ctypes.addressof(out), 1, 0, 0, None, None)
+    assert st == _lib.RNS_E_NODEVICE
     p = ctypes.c_void_p()
     assert lib.rns_host_ctx_create(0, 1 << 20, 2, ctypes.byref(p)) == _lib.RNS_E_NODEVICE
     assert lib.rns_fill_splitmix64_dev(fake, 64, 1, None) == _lib.RNS_E_NODEVICE
