@@ -116,6 +116,30 @@ int main(void)
         for (uint32_t i = 0; i < n; ++i)
             CHECK(got[i] == want[i], "device batch (hint %u) packet %u: %04x != %04x", hints[h], i, got[i], want[i]);
     }
+    /* compact descriptors: the same batch with 32-bit offsets */
+    {
+        uint32_t *off32 = malloc(n * sizeof *off32), *d_off32 = NULL;
+        for (uint32_t i = 0; i < n; ++i)
+            off32[i] = (uint32_t)off[i];
+        HIP_OK(hipMalloc((void **)&d_off32, n * sizeof *off32));
+        HIP_OK(hipMemcpy(d_off32, off32, n * sizeof *off32, hipMemcpyHostToDevice));
+        for (int h = 0; h < 3; ++h) {
+            HIP_OK(hipMemset(d_out, 0, n * sizeof *got));
+            CHECK(rns_csum_batch_dev_off32(d_arena, bytes, d_off32, d_len, d_seed, d_out, n, RNS_FLAG_COMPLEMENT,
+                                           hints[h], d_bad, st) == RNS_OK,
+                  "rns_csum_batch_dev_off32 hint %u", hints[h]);
+            HIP_OK(hipStreamSynchronize(st));
+            HIP_OK(hipMemcpy(got, d_out, n * sizeof *got, hipMemcpyDeviceToHost));
+            for (uint32_t i = 0; i < n; ++i)
+                CHECK(got[i] == want[i], "compact batch (hint %u) packet %u: %04x != %04x", hints[h], i, got[i],
+                      want[i]);
+        }
+        CHECK(rns_csum_batch_dev_off32(d_arena, bytes, NULL, d_len, d_seed, d_out, n, 0, 0, NULL, st) ==
+                  RNS_E_INVALID,
+              "NULL compact offsets");
+        hipFree(d_off32);
+        free(off32);
+    }
     uint32_t bad = 1;
     HIP_OK(hipMemcpy(&bad, d_bad, sizeof bad, hipMemcpyDeviceToHost));
     CHECK(bad == 0, "d_bad = %u", bad);
