@@ -110,8 +110,9 @@ int rns_csum_batch_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
                        const uint32_t *d_len, const uint16_t *d_seed, uint16_t *d_out, uint32_t n,
                        uint32_t flags, uint32_t len_hint, uint32_t *d_bad, void *stream);
 
-/* Compact descriptors: as rns_csum_batch_dev with 32-bit packet offsets (arenas
- * below 4 GiB), 10 B of descriptors per packet instead of 14.  Same results. */
+/* Compact descriptors: as rns_csum_batch_dev (util.rs:88-110 per packet) with
+ * 32-bit packet offsets (arenas below 4 GiB), 10 B of descriptors per packet
+ * instead of 14.  Same results. */
 int rns_csum_batch_dev_off32(const uint8_t *d_arena, uint64_t arena_bytes, const uint32_t *d_off32,
                              const uint32_t *d_len, const uint16_t *d_seed, uint16_t *d_out, uint32_t n,
                              uint32_t flags, uint32_t len_hint, uint32_t *d_bad, void *stream);
