@@ -12,7 +12,19 @@ ranks / max-over-ranks wall time of the K timed steps / 2^30.
         --master-port P bench.py --gpus N --steps K --warmup W
 
 Packets shard trivially: every rank checksums its own batch with
-no data-path collective ("scaling": "weak").  Rank 0 prints one JSON line.
+no data-path collective ("scaling": "weak"), so `value` is the compute-only
+aggregate.  At N>1 the line also carries the §8(e) collective leg measured
+separately: `value_gather` = the same steps with one RCCL all-gather of every
+rank's u16 results (as uint8, 2 B per packet) per step, and `gather_ms` = the
+all-gather alone.  Rank 0 prints one JSON line.
+
+Kernel time: one event pair around the K back-to-back timed launches gives the
+per-launch mean (`kernel_avg_us`) from which `roofline.frac` is computed.  A
+rocprofv3 --kernel-trace of the same command reproduces it (tools/profile_bench.py
+reports the trace's per-dispatch mean and median of the same K launches).  Event
+pairs around single launches are NOT used for the figure: each pair measured
+≈5 µs above the dispatch rocprof records (profiles/r02_evpair_vs_rocprof_c3_1500B.json);
+`--median-launches N` still reports their median as a diagnostic.
 """
 from __future__ import annotations
 
@@ -43,15 +55,20 @@ def parse_args(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample duration (single thread)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-pipeline", action="store_true", help="skip the PCIe-inclusive extra measurement")
-    p.add_argument("--gather", action="store_true",
-                   help="add an RCCL all_gather of every rank's results to each step (not the default: "
-                        "the stack consumes results where they are produced)")
+    p.add_argument("--no-gather", action="store_true",
+                   help="N>1: skip the compute+all-gather and gather-only legs (value is compute-only either way)")
+    p.add_argument("--median-launches", type=int, default=0,
+                   help="diagnostic: N extra launches each inside its own event pair, median reported "
+                        "(pairs add ~5 us per launch; 0 = skip)")
     p.add_argument("--scaling", choices=("auto", "weak", "strong"), default="auto",
                    help="weak: every rank checksums a full batch of the config; strong: the config's batch is "
                         "sharded by packet index across ranks (auto: strong for c5_imix, whose BASELINE.json "
                         "config is one 8M-packet batch over 8 GPUs; weak otherwise)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_{config}.json"))
-    return p.parse_args(argv)
+    args = p.parse_args(argv)
+    if args.shape and args.desc == "32":
+        p.error("--shape overrides take 64-bit descriptors (--desc 64 or auto)")
+    return args
 
 
 # ---------------------------------------------------------------------------
@@ -105,20 +122,22 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def timed_loop(engine, dist: Dist, steps: int, warmup: int) -> dict:
+def timed_loop(engine, dist: Dist, steps: int, warmup: int, step=None) -> dict:
     """W untimed steps, then exactly K steps bracketed by sync + barrier on both
     sides; wall time is the max over ranks.  Device time per launch = one pair of
     events on the launch stream around the K back-to-back launches, / K (events
-    between launches would insert ~10 µs gaps: see DESIGN.md, measurement)."""
+    between launches would insert ~10 µs gaps: see DESIGN.md, measurement).
+    `step` (default engine.step) is what one step runs."""
+    step = step or engine.step
     for _ in range(warmup):
-        engine.step()
+        step()
     engine.sync()
     dist.barrier()
     engine.sync()
     t0 = time.perf_counter()
     engine.begin_timing()
     for _ in range(steps):
-        engine.step()
+        step()
     engine.end_timing(steps)
     engine.sync()
     dist.barrier()
@@ -128,12 +147,69 @@ def timed_loop(engine, dist: Dist, steps: int, warmup: int) -> dict:
             "kernel_ms": engine.kernel_ms()}
 
 
+class ResultGather:
+    """SURVEY §8(e)'s collective: every rank's per-packet u16 results all-gathered
+    to every rank, sent as uint8 (RCCL has no 16-bit unsigned type: ncclUint8 with
+    2·n bytes per rank; gloo has no int16 either).  Ranks with fewer packets (strong
+    scaling of a batch that does not divide evenly) pad to the largest shard; the
+    counts are all-gathered once so `results()` rebuilds the global order."""
+
+    def __init__(self, dist: Dist, n_local: int, device):
+        import torch
+        self.dist, self.torch = dist, torch
+        self.n_local = int(n_local)
+        self.n_max = int(dist.max(float(n_local)))
+        self.counts = [int(c) for c in self._counts()]
+        # gloo (CPU tests, one-GPU rehearsals) moves host tensors: stage through CPU there
+        self.host_staged = dist.enabled and dist.backend != "nccl" and torch.device(device).type == "cuda"
+        bufdev = "cpu" if self.host_staged else device
+        self.send = torch.zeros(2 * self.n_max, dtype=torch.uint8, device=bufdev)
+        self.recv = torch.empty(2 * self.n_max * dist.world, dtype=torch.uint8, device=bufdev)
+
+    def _counts(self):
+        if not self.dist.enabled:
+            return [self.n_local]
+        t = self.torch.tensor([self.n_local], dtype=self.torch.int64,
+                              device=self.send_device() if self.dist.backend == "nccl" else "cpu")
+        out = [self.torch.zeros_like(t) for _ in range(self.dist.world)]
+        self.dist.dist.all_gather(out, t)
+        return [int(x.item()) for x in out]
+
+    def send_device(self):
+        return f"cuda:{self.dist.local_rank}"
+
+    @property
+    def bytes_per_rank(self) -> int:
+        return 2 * self.n_max
+
+    def __call__(self, out_u16):
+        src = out_u16.view(self.torch.uint8)
+        if self.host_staged:
+            src = src.cpu()
+        if self.n_local == self.n_max:
+            send = src
+        else:
+            self.send[:src.numel()].copy_(src)
+            send = self.send
+        if self.dist.enabled:
+            self.dist.dist.all_gather_into_tensor(self.recv, send)
+        else:
+            self.recv.copy_(send)
+        return self.recv
+
+    def results(self):
+        """The gathered u16 results of all ranks, rank order, padding removed (numpy)."""
+        import numpy as np
+        raw = self.recv.cpu().numpy().view(np.uint16).reshape(self.dist.world, self.n_max)
+        return np.concatenate([raw[r, :c] for r, c in enumerate(self.counts)])
+
+
 # ---------------------------------------------------------------------------
 # GPU engine: the product path
 # ---------------------------------------------------------------------------
 class GpuEngine:
-    def __init__(self, config: str, rank: int, local_rank: int, shape=None, gather_dist: Dist | None = None,
-                 steps: int = 0, world: int = 1, strong: bool = False, compact="64"):
+    def __init__(self, config: str, rank: int, local_rank: int, shape=None, steps: int = 0, world: int = 1,
+                 strong: bool = False, compact="64"):
         import torch
 
         from rustnetworkstack_amd.workloads import DATA_SEED, DeviceBatch, make_layout
@@ -160,13 +236,11 @@ class GpuEngine:
         self.compact = compact in (True, "32")
         for b in self.batches:  # bind every rotating batch (and upload compact offsets) before any timing
             b.launcher(complement=True, shape=shape, compact=self.compact)
-        self.gather = gather_dist
         self.k = 0
+        self.last = self.batches[0]
         self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         self.timed = 0
-        if gather_dist is not None and gather_dist.enabled:
-            n = self.layout.n
-            self.gathered = torch.empty(n * gather_dist.world, dtype=torch.int16, device=self.device)
+        self.gatherer = None
         torch.cuda.synchronize()
 
     @property
@@ -181,8 +255,29 @@ class GpuEngine:
         b = self.batches[self.k % len(self.batches)]
         self.k += 1
         b.launcher(complement=True, shape=self.shape, compact=self.compact)()  # pre-bound: one ctypes call
-        if self.gather is not None and self.gather.enabled:
-            self.gather.dist.all_gather_into_tensor(self.gathered, b.out.view(self.torch.int16))
+        self.last = b
+
+    def gather(self):
+        """The all-gather of the results of the batch the last step checksummed."""
+        return self.gatherer(self.last.out)
+
+    def step_and_gather(self):
+        self.step()
+        self.gather()
+
+    def per_launch_us(self, count: int) -> list:
+        """`count` launches, each bracketed by its own event pair on the launch stream
+        (the rocprof-style per-dispatch duration; the gaps these events put BETWEEN
+        launches are outside every pair)."""
+        torch = self.torch
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(count)]
+        self.sync()
+        for a, b in evs:
+            a.record()
+            self.step()
+            b.record()
+        self.sync()
+        return [1e3 * a.elapsed_time(b) for a, b in evs]
 
     def sync(self):
         self.torch.cuda.synchronize()
@@ -211,37 +306,80 @@ class GpuEngine:
 # ---------------------------------------------------------------------------
 # CPU baseline: the reference's algorithm (oracle/ restatement), host cores
 # ---------------------------------------------------------------------------
-def cpu_baseline(engine: GpuEngine, seconds: float) -> dict:
+def cpu_grant() -> dict:
+    """CPUs this process may actually use: the affinity mask, capped by a cgroup CPU
+    quota when one is set (a gpurun box shows the whole machine in its mask but
+    grants a share of it through cpu.max)."""
+    visible = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                parts = f.read().split()
+        except OSError:
+            continue
+        if path.endswith("cpu.max"):
+            if parts and parts[0] != "max":
+                quota = float(parts[0]) / float(parts[1] if len(parts) > 1 else 100000)
+        else:
+            try:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    period = float(f.read().strip())
+                q = float(parts[0])
+                if q > 0:
+                    quota = q / period
+            except (OSError, ValueError, IndexError):
+                pass
+        break
+    threads = visible if quota is None else max(1, min(visible, int(quota + 0.5)))
+    return {"visible": visible, "quota_cpus": quota, "threads": threads}
+
+
+def cpu_baseline(engine: GpuEngine, seconds: float, sample_min_bytes: int = 512 << 20,
+                 sample_max_bytes: int = 3 << 30) -> dict:
     """Times the literal C restatement of util.rs:88-106 (oracle/csum_oracle.c,
-    gcc -O3, baseline x86-64) on a bounded sample of the same batch: single
-    thread for `seconds`, all host cores for a quarter of that.  Also checks
-    the GPU results of the sample packets against it."""
+    gcc -O3, baseline x86-64 — gcc auto-vectorises its loop; it is not the Rust
+    build, which this image cannot compile) on the same batches the GPU reads:
+    whole batches, at least `sample_min_bytes` (larger than the host's L3, so the
+    CPU reads DRAM like the GPU reads HBM) and at most `sample_max_bytes`.  Run on
+    every CPU the process is granted (`value`) and on one thread (`value_1_thread`).
+    Also checks the GPU results of every sampled packet against it."""
     import numpy as np
 
     from oracle.oracle import get_oracle
     orc = get_oracle()
-    lay = engine.layout
-    # sample: the first packets of the batch, ~64 MiB of payload
-    count = int(min(lay.n, max(1, (64 << 20) // max(int(lay.mean_len), 1))))
-    end = int(lay.off[count - 1] + lay.length[count - 1])
-    arena = engine.batches[0].arena[:end].cpu().numpy()
-    off, ln, sd = lay.off[:count], lay.length[:count], lay.seed[:count]
-    sample_bytes = int(ln.astype(np.uint64).sum())
+    grant = cpu_grant()
+    samples, total = [], 0
+    for b in engine.batches:  # rotating batches (c2) each bring their own bytes
+        lay = b.layout
+        if samples and total + lay.arena_bytes > sample_max_bytes:
+            break
+        arena = b.arena[:lay.arena_bytes].cpu().numpy()
+        samples.append((b, arena, lay))
+        total += lay.payload_bytes
+        if total >= sample_min_bytes:
+            break
+    sample_bytes = sum(lay.payload_bytes for _, _, lay in samples)
+    arena_bytes = sum(lay.arena_bytes for _, _, lay in samples)
+
+    def one_pass(threads: int):
+        return [orc.batch(arena, lay.off, lay.length, lay.seed, complement=True, threads=threads, check=False)
+                for _, arena, lay in samples]
 
     def rate(threads: int, budget: float):
         passes, t0 = 0, time.perf_counter()
         while True:
-            res = orc.batch(arena, off, ln, sd, complement=True, threads=threads)
+            res = one_pass(threads)
             passes += 1
             dt = time.perf_counter() - t0
             if dt >= budget:
                 return sample_bytes * passes / dt / 2 ** 30, res, passes, dt
 
-    v1, res, passes, dt = rate(1, seconds)
-    box_cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    mt = int(min(16, box_cores))   # gpurun boxes grant 16 CPUs; cpu_count() shows the whole machine
-    vmt, _, _, _ = rate(mt, max(seconds / 4, 1.0))
-    gpu = engine.out_sample(count)
+    vmt, res, passes_mt, dt_mt = rate(grant["threads"], max(seconds / 2, 1.0))
+    v1, res1, passes1, dt1 = rate(1, seconds)
+    exact = all(np.array_equal(b.out.view(engine.torch.int16).cpu().numpy().view(np.uint16), r)
+                for (b, _, _), r in zip(samples, res))
+    exact = exact and all(np.array_equal(a, c) for a, c in zip(res, res1))
     ns_zero = orc.time_ones_comp(bytes(512), 2_000_000)
     ns_ff = orc.time_ones_comp(b"\xff" * 512, 2_000_000)
     cpu_model = ""
@@ -250,15 +388,21 @@ def cpu_baseline(engine: GpuEngine, seconds: float) -> dict:
             cpu_model = next((ln_.split(":", 1)[1].strip() for ln_ in f if ln_.startswith("model name")), "")
     except OSError:
         pass
+    n_pk = sum(lay.n for _, _, lay in samples)
     return {
-        "value": round(v1, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-        "sample": f"first {count} packets ({sample_bytes} B) of the {lay.name} batch, "
-                  f"{passes} passes in {dt:.1f} s; oracle/csum_oracle.c literal util.rs:88-106 loop, gcc -O3",
-        "value_all_cores": round(vmt, 3), "all_cores_threads": mt,
+        "value": round(vmt, 3), "unit": "GiB/s", "cores": grant["threads"], "kind": "port",
+        "sample": f"{len(samples)} whole {engine.layout.name} batch(es): {n_pk} packets, {sample_bytes} B of payload "
+                  f"in {arena_bytes} B of arena (> host L3: read from DRAM); {grant['threads']} threads x "
+                  f"{passes_mt} passes in {dt_mt:.1f} s, 1 thread x {passes1} passes in {dt1:.1f} s",
+        "what": "gcc -O3 restatement of util.rs:88-106 (oracle/csum_oracle.c, baseline x86-64; gcc auto-vectorises "
+                "the loop), not the Rust build (no cargo/rustc in the image); packets partitioned by index over threads",
+        "value_1_thread": round(v1, 3),
+        "threads_granted": grant["threads"], "host_cpus_visible": grant["visible"],
+        "cgroup_cpu_quota": grant["quota_cpus"],
         "util_bench_ns_per_iter": {"compute_ones_comp_512B_zeros": round(ns_zero, 2),
                                    "compute_ones_comp_512B_0xff": round(ns_ff, 2)},
-        "host_cpu": cpu_model, "host_cpus_visible": box_cores,
-        "gpu_sample_bit_exact": bool(np.array_equal(gpu, res)),
+        "host_cpu": cpu_model,
+        "gpu_sample_bit_exact": bool(exact),
     }
 
 
@@ -299,17 +443,20 @@ def main(argv=None):
     dist = Dist()
     shape = tuple(int(x) for x in args.shape.split(",")) if args.shape else None
     strong = args.scaling == "strong" or (args.scaling == "auto" and args.config == "c5_imix")
-    engine = GpuEngine(args.config, dist.rank, dist.local_rank, shape=shape,
-                       gather_dist=dist if args.gather else None, steps=args.steps, world=dist.world, strong=strong,
-                       compact=args.desc)
+    engine = GpuEngine(args.config, dist.rank, dist.local_rank, shape=shape, steps=args.steps, world=dist.world,
+                       strong=strong, compact=args.desc)
     r = timed_loop(engine, dist, args.steps, args.warmup)
     elapsed = r["elapsed_s"]
     # all ranks' payload (strong: the shards add up to the config's one batch)
-    total_bytes = int(dist.sum(engine.payload_bytes)) * args.steps
+    step_bytes = int(dist.sum(engine.payload_bytes))
+    total_bytes = step_bytes * args.steps
     value = total_bytes / elapsed / 2 ** 30
     kernel_ms = r["kernel_ms"]
+    per = engine.per_launch_us(args.median_launches) if args.median_launches > 0 else []
     algo_bytes = engine.payload_bytes + 2 * engine.n
-    achieved = algo_bytes / (kernel_ms * 1e-3) / 1e9
+    desc_bytes = engine.n * ((4 if engine.compact else 8) + 4 + 2)
+    kernel_us = kernel_ms * 1e3
+    achieved = algo_bytes / (kernel_us * 1e-6) / 1e9
     traffic = load_traffic(args.traffic_json, args.config)
     line = {
         "metric": METRIC,
@@ -330,8 +477,7 @@ def main(argv=None):
             "packets_per_gpu": engine.n,
             "payload_bytes_per_gpu": engine.payload_bytes,
             "batch": "one batch sharded by packet index across ranks" if strong else "a full batch per rank",
-            "parallelism": f"packet shards x{dist.world}, no data-path collective"
-                           + (" + RCCL all_gather of results" if args.gather else ""),
+            "parallelism": f"packet shards x{dist.world}, no data-path collective in `value`",
             "kernel_shape": list(shape) if shape else "auto",
             "descriptors": ("u32 offset + u32 length + u16 seed (rns_csum_batch_dev_off32)" if engine.compact
                             else "u64 offset + u32 length + u16 seed (rns_csum_batch_dev)"),
@@ -345,12 +491,31 @@ def main(argv=None):
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
             "kernel": engine.kernel_name() if shape is None else f"shape {list(shape)}",
-            "kernel_avg_us": round(kernel_ms * 1e3, 2),
+            "kernel_avg_us": round(kernel_us, 2),
+            "frac_from": "kernel_avg_us: one event pair (launch stream) around the K back-to-back timed launches / K",
             "algorithmic_bytes_per_launch": algo_bytes,
+            "descriptor_bytes_per_launch": desc_bytes,
+            "frac_incl_descriptors": round((algo_bytes + desc_bytes) / (kernel_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
             "traffic_source": (traffic or {}).get("source"),
         },
         "cpu_baseline": None,
     }
+    if per:
+        srt = sorted(per)
+        line["roofline"]["evpair_median_us"] = round(srt[len(srt) // 2], 2)
+        line["roofline"]["evpair_launches"] = len(per)
+    if dist.world > 1 and not args.no_gather:
+        # the same steps plus one all-gather of every rank's results, and the gather alone
+        engine.gatherer = ResultGather(dist, engine.n, engine.device)
+        rg = timed_loop(engine, dist, args.steps, args.warmup, step=engine.step_and_gather)
+        rgo = timed_loop(engine, dist, args.steps, args.warmup, step=engine.gather)
+        line["value_compute"] = line["value"]
+        line["value_gather"] = round(total_bytes / rg["elapsed_s"] / 2 ** 30, 2)
+        line["ms_per_step_gather"] = round(rg["elapsed_s"] * 1e3 / args.steps, 4)
+        line["gather_ms"] = round(rgo["elapsed_s"] * 1e3 / args.steps, 4)
+        line["gather"] = {"collective": f"all_gather_into_tensor ({dist.backend}) of uint8 results",
+                          "bytes_per_rank": engine.gatherer.bytes_per_rank,
+                          "bytes_received_per_rank": engine.gatherer.bytes_per_rank * (dist.world - 1)}
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(engine, args.cpu_seconds)
     if dist.rank == 0 and dist.world == 1 and not args.no_host_pipeline:

@@ -207,6 +207,9 @@ int rns_csum_batch_dev_cfg(const uint8_t *d_arena, uint64_t arena_bytes, const u
 /* Host-resident batch through a staging context: chunked H2D copies, kernels and
  * D2H copies of the 2-byte results overlapped on several streams of `device`.
  * Offsets must be ascending.  Synchronous (returns when h_out is filled).
+ * The whole batch is validated before anything is queued: a packet with
+ * (offset mod 256) + length > chunk_bytes returns RNS_E_TOOLARGE (and out-of-arena /
+ * descending descriptors RNS_E_BOUNDS / RNS_E_ORDER) with h_out untouched.
  * For full PCIe rate allocate h_arena with rns_host_alloc (pinned).  A context
  * serialises its own calls (internal mutex); use one per thread for concurrency. */
 typedef struct rns_host_ctx rns_host_ctx;
@@ -251,7 +254,9 @@ int rns_csum_batch_multi_dev(const rns_dev_batch *batches, uint32_t nbatches, ui
  * send_packet netif.rs:85-98 -> tun_send tun.c:88-90).  rns_io_recv_batch waits up
  * to timeout_ms for the first datagram, then reads every datagram already queued
  * (up to max_pkts) into consecutive slot_bytes slots of h_arena (2048 = the
- * reference's MRU, netif.rs:66); h_off/h_len describe them.  Returns the number of
+ * reference's MRU, netif.rs:66); h_off/h_len describe them.  A datagram longer
+ * than its slot is dropped (on socket fds recv(MSG_TRUNC) reports its full length),
+ * never handed on truncated; max_pkts is capped at INT_MAX.  Returns the number of
  * datagrams (0 on timeout) or RNS_E_IO.  Works on a TUN fd or any datagram fd.
  * rns_io_send_batch writes n datagrams; returns how many were written. */
 int rns_io_recv_batch(int fd, uint8_t *h_arena, uint64_t slot_bytes, uint32_t max_pkts, uint64_t *h_off,

@@ -50,19 +50,20 @@ class PreparedBatch:
     ``shape`` = (variant, lanes_per_packet, unroll, max_blocks) overrides the
     automatic kernel shape (tuning); see rns_csum_batch_dev_cfg.
 
-    ``off`` is int64, or int32 for the compact descriptor form
-    (rns_csum_batch_dev_off32: the tensor holds unsigned 32-bit offsets, arenas
-    below 4 GiB; 10 B of descriptors per packet instead of 14).
+    ``compact=True`` selects the compact descriptor form explicitly
+    (rns_csum_batch_dev_off32): ``off`` is then an int32 tensor whose bits are
+    UNSIGNED 32-bit offsets (arenas below 4 GiB; 10 B of descriptors per packet
+    instead of 14).  Otherwise ``off`` must be int64; an int32 ``off`` without
+    ``compact=True`` is a TypeError, never a silent switch of the descriptor form.
     """
 
     def __init__(self, arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor,
                  seed: torch.Tensor | None = None, *, complement: bool = False, out: torch.Tensor | None = None,
                  len_hint: int = 0, bad: torch.Tensor | None = None,
-                 shape: tuple[int, int, int, int] | None = None):
+                 shape: tuple[int, int, int, int] | None = None, compact: bool = False):
         _require_cuda(arena, "arena", (torch.uint8,))
-        _require_cuda(off, "off", (torch.int64, torch.int32))
+        _require_cuda(off, "off", (torch.int32,) if compact else (torch.int64,))
         _require_cuda(length, "length", (torch.int32,))
-        compact = off.dtype == torch.int32
         if compact and shape is not None:
             raise ValueError("shape overrides take 64-bit offsets")
         n = off.numel()
@@ -125,18 +126,20 @@ class PreparedBatch:
 
 def csum_batch(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, seed: torch.Tensor | None = None,
                *, complement: bool = False, out: torch.Tensor | None = None, len_hint: int = 0,
-               bad: torch.Tensor | None = None, shape: tuple[int, int, int, int] | None = None) -> torch.Tensor:
+               bad: torch.Tensor | None = None, shape: tuple[int, int, int, int] | None = None,
+               compact: bool = False) -> torch.Tensor:
     """Checksum every packet of a device-resident batch; returns uint16 [n] on the same device.
 
     Launches on the current torch stream of ``arena``'s device and returns
     without synchronising.  A packet outside the arena yields 0 and increments
     ``bad`` (int32 [1] device tensor) if given.  ``shape`` = (variant,
     lanes_per_packet, unroll, max_blocks) overrides the kernel shape (tuning).
+    ``compact=True``: ``off`` holds unsigned 32-bit offsets in an int32 tensor.
     """
     _require_cuda(arena, "arena", (torch.uint8,))
     with torch.cuda.device(arena.device):
         return PreparedBatch(arena, off, length, seed, complement=complement, out=out, len_hint=len_hint, bad=bad,
-                             shape=shape)()
+                             shape=shape, compact=compact)()
 
 
 def csum_batch_strided(arena: torch.Tensor, n: int, stride: int, length: int, *, first_off: int = 0,

@@ -8,7 +8,9 @@
 #include <cerrno>
 #include <cstdint>
 #include <fcntl.h>
+#include <climits>
 #include <poll.h>
+#include <sys/socket.h>
 #include <sys/uio.h>
 #include <unistd.h>
 
@@ -21,6 +23,8 @@ int rns_io_recv_batch(int fd, uint8_t *h_arena, uint64_t slot_bytes, uint32_t ma
 {
     if (fd < 0 || !h_arena || !h_off || !h_len || slot_bytes == 0 || max_pkts == 0)
         return RNS_E_INVALID;
+    if (max_pkts > static_cast<uint32_t>(INT_MAX))  // the count is returned as an int
+        max_pkts = static_cast<uint32_t>(INT_MAX);
     struct pollfd pfd = {fd, POLLIN, 0};
     int pr;
     do {
@@ -38,9 +42,19 @@ int rns_io_recv_batch(int fd, uint8_t *h_arena, uint64_t slot_bytes, uint32_t ma
         return RNS_E_IO;
     uint32_t n = 0;
     int status = 0;
+    bool sock = true;  // socket fds: recv(MSG_TRUNC) reports a datagram's full length
     while (n < max_pkts) {
         uint8_t *slot = h_arena + static_cast<uint64_t>(n) * slot_bytes;
-        const ssize_t r = read(fd, slot, slot_bytes);  // one datagram per read, like tun_recv
+        ssize_t r;
+        if (sock) {
+            r = recv(fd, slot, slot_bytes, MSG_TRUNC);
+            if (r < 0 && errno == ENOTSOCK) {
+                sock = false;
+                continue;
+            }
+        } else {
+            r = read(fd, slot, slot_bytes);  // one datagram per read, like tun_recv
+        }
         if (r < 0) {
             if (errno == EINTR)
                 continue;
@@ -50,6 +64,8 @@ int rns_io_recv_batch(int fd, uint8_t *h_arena, uint64_t slot_bytes, uint32_t ma
         }
         if (r == 0)  // peer closed (socket fds)
             break;
+        if (static_cast<uint64_t>(r) > slot_bytes)  // longer than its slot: dropped, never
+            continue;                               // handed on truncated (its slot is reused)
         h_off[n] = static_cast<uint64_t>(n) * slot_bytes;
         h_len[n] = static_cast<uint32_t>(r);
         ++n;

@@ -1792,12 +1792,17 @@ int rns_csum_batch_host(rns_host_ctx *ctx, const uint8_t *h_arena, uint64_t aren
         return RNS_OK;
     if (!h_arena || !h_off || !h_len || !h_out)
         return RNS_E_INVALID;
-    // Validate the whole batch first so a bad descriptor never reaches the device.
+    // Validate the whole batch first so a bad descriptor never reaches the device and
+    // nothing is queued for a batch that cannot finish.  A chunk starts at its first
+    // packet's offset rounded down to 256 bytes, so a packet fits a staging chunk iff
+    // (off mod 256) + len <= chunk_bytes.
     for (uint32_t i = 0; i < n; ++i) {
         if (h_off[i] > arena_bytes || h_len[i] > arena_bytes - h_off[i])
             return RNS_E_BOUNDS;
         if (i && h_off[i] < h_off[i - 1])
             return RNS_E_ORDER;
+        if ((h_off[i] & 255u) + h_len[i] > ctx->chunk_bytes)
+            return RNS_E_TOOLARGE;
     }
     std::lock_guard<std::mutex> lock(ctx->mu);
     int st = hip_status(hipSetDevice(ctx->device));
@@ -1818,8 +1823,10 @@ int rns_csum_batch_host(rns_host_ctx *ctx, const uint8_t *h_arena, uint64_t aren
             hi = end;
             ++i1;
         }
-        if (i1 == i0)
-            return RNS_E_TOOLARGE;
+        if (i1 == i0) {  // (excluded by the validation pass; never leave queued slots undrained)
+            st = RNS_E_TOOLARGE;
+            break;
+        }
         auto &s = ctx->slots[k++ % nslots];
         st = drain_slot(s, h_out);
         if (st)

@@ -144,7 +144,8 @@ class DeviceBatch:
                     raise ValueError("compact descriptors need an arena below 4 GiB")
                 off = torch.from_numpy(self.layout.off.astype(np.uint32).view(np.int32)).to(self.device)
             self._prepared[key] = PreparedBatch(self.arena, off, self.length, self.seed, complement=complement,
-                                                out=self.out, len_hint=int(round(self.layout.mean_len)), shape=shape)
+                                                out=self.out, len_hint=int(round(self.layout.mean_len)), shape=shape,
+                                                compact=compact)
         return self._prepared[key]
 
     def run(self, complement: bool = False, shape=None):

@@ -1,12 +1,16 @@
-"""The N>1 bench path (bench.py's Dist + timed_loop: barriers, max-over-ranks wall
-time, weak-scaling aggregation) with world_size 2 over gloo on CPU.  The GPU
+"""The N>1 bench path with world_size 2 over gloo on CPU: bench.py's own main()
+(Dist, timed_loop, the byte aggregation, the §8(e) all-gather leg through
+ResultGather, value_compute / value_gather / gather_ms in the line).  The GPU
 engine is replaced by a CPU engine that checksums each rank's shard with the
-oracle (tests may use the oracle); the harness code is bench.py's own."""
+oracle (tests may use the oracle); everything else is bench.py's code.  The
+all-gathered results of both ranks must equal the oracle over the whole batch."""
 import json
 import os
 import socket
 import subprocess
 import sys
+
+import pytest
 
 from conftest import ROOT
 
@@ -14,43 +18,63 @@ WORKER = r'''
 import json, os, sys, time
 sys.path.insert(0, {root!r})
 import numpy as np
+import torch
 import bench
 from oracle.oracle import get_oracle, splitmix64_bytes
 from rustnetworkstack_amd.workloads import make_layout
 
-class CpuEngine:
-    """Stand-in for bench.GpuEngine: same interface, oracle compute."""
-    def __init__(self, rank, world):
-        self.layout = make_layout("c5_imix", n=40000, shard=(rank, world))
+N = {n}
+ENGINES = []
+
+class _Batch:
+    def __init__(self, layout):
+        self.layout = layout
+        self.out = torch.zeros(layout.n, dtype=torch.uint16)
+
+class CpuEngine(bench.GpuEngine):
+    """Stand-in for bench.GpuEngine: same interface, oracle compute on CPU tensors."""
+    def __init__(self, config, rank, local_rank, shape=None, steps=0, world=1, strong=False, compact="64"):
+        self.torch = torch
+        self.device = torch.device("cpu")
+        if strong:
+            self.layout = make_layout(config, n=N, shard=(rank, world))
+        else:
+            self.layout = make_layout(config, n=N, data_seed=0x5EEDC0DE + 0x1000 * rank)
         self.arena = splitmix64_bytes(self.layout.data_seed, self.layout.arena_bytes)
+        self.batches = [_Batch(self.layout)]
+        self.last = self.batches[0]
+        self.compact, self.shape, self.k, self.timed = True, None, 0, 0
+        self.gatherer = None
         self.orc = get_oracle()
-        self.times = []
-        self.out = None
-    n = property(lambda s: s.layout.n)
-    payload_bytes = property(lambda s: s.layout.payload_bytes)
+        ENGINES.append(self)
     def step(self):
-        self.out = self.orc.batch(self.arena, self.layout.off, self.layout.length, self.layout.seed, complement=True)
+        res = self.orc.batch(self.arena, self.layout.off, self.layout.length, self.layout.seed, complement=True)
+        self.last.out.copy_(torch.from_numpy(res))
     def sync(self):
         pass
     def begin_timing(self):
         self.t0 = time.perf_counter()
     def end_timing(self, steps):
         self.ms = 1e3 * (time.perf_counter() - self.t0) / steps
+        self.timed = steps
     def kernel_ms(self):
         return self.ms
+    def per_launch_us(self, count):
+        out = []
+        for _ in range(count):
+            t0 = time.perf_counter(); self.step(); out.append(1e6 * (time.perf_counter() - t0))
+        return out
+    def kernel_name(self):
+        return "cpu stand-in"
 
-d = bench.Dist(backend="gloo")
-eng = CpuEngine(d.rank, d.world)
-r = bench.timed_loop(eng, d, steps=3, warmup=1)
-# ranks' results, gathered to check the shards tile the whole batch
-import torch, torch.distributed as dist
-outs = [torch.zeros(0) for _ in range(d.world)]
-obj = [None] * d.world
-dist.all_gather_object(obj, (d.rank, eng.n, eng.out.tolist(), r["local_elapsed_s"], r["elapsed_s"],
-                             d.sum(eng.payload_bytes)))
-if d.rank == 0:
-    print(json.dumps(obj))
-d.close()
+bench.GpuEngine = CpuEngine
+line = bench.main(["--config", {config!r}, "--steps", "3", "--warmup", "1", "--median-launches", "3",
+                   "--traffic-json", "/nonexistent/{{config}}.json"])
+eng = ENGINES[0]
+rank = int(os.environ["RANK"])
+with open(os.path.join({outdir!r}, f"rank{{rank}}.json"), "w") as f:   # (stdout lines of 2 ranks interleave)
+    json.dump({{"rank": rank, "line": line, "n": eng.n, "counts": eng.gatherer.counts,
+               "gathered": eng.gatherer.results().tolist()}}, f)
 '''
 
 
@@ -62,30 +86,54 @@ def free_port():
     return p
 
 
-def test_two_rank_gloo_harness(tmp_path, oracle):
+@pytest.mark.parametrize("config,n", [("c5_imix", 40001), ("c3_1500B", 3000)])
+def test_two_rank_gloo_bench_main(tmp_path, oracle, config, n):
     script = tmp_path / "worker.py"
-    script.write_text(WORKER.format(root=ROOT))
+    script.write_text(WORKER.format(root=ROOT, n=n, config=config, outdir=str(tmp_path)))
     env = dict(os.environ, OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(script)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
-    line = [ln for ln in r.stdout.splitlines() if ln.startswith("[[")][-1]
-    ranks = json.loads(line)
-    # the max-over-ranks time every rank reports is the same and >= each local time
-    assert len({round(x[4], 9) for x in ranks}) == 1
-    assert all(x[4] >= x[3] - 1e-9 for x in ranks)
-    # shards by packet index tile the full batch, and each rank's results are the oracle's
+    res = {}
+    for rank in (0, 1):
+        with open(tmp_path / f"rank{rank}.json") as f:
+            res[rank] = json.load(f)
+    printed = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(printed) == 1                           # rank 0 prints one JSON line
+    line = printed[0]
+    assert line == res[0]["line"]
+    assert line["n_gpus"] == 2
     import numpy as np
 
     from oracle.oracle import splitmix64_bytes
     from rustnetworkstack_amd.workloads import make_layout
-    total = sum(x[1] for x in ranks)
-    assert total == 40000
-    # strong scaling's aggregate: the shards' payload adds up to the one batch's, on every rank
-    assert {x[5] for x in ranks} == {make_layout("c5_imix", n=40000).payload_bytes}
-    for rank, n, out, _, _, _ in ranks:
-        lay = make_layout("c5_imix", n=40000, shard=(rank, 2))
+    strong = config == "c5_imix"
+    assert line["scaling"] == ("strong" if strong else "weak")
+    # the §8(e) legs: compute-only value, compute+gather, gather alone
+    for k in ("value_compute", "value_gather", "ms_per_step_gather", "gather_ms"):
+        assert k in line and line[k] > 0, k
+    assert line["value_compute"] == line["value"]
+    # aggregate bytes: strong = the shards add up to the one batch; weak = one full batch per rank
+    whole = make_layout(config, n=n).payload_bytes
+    per_rank = [res[r]["n"] for r in (0, 1)]
+    if strong:
+        assert sum(per_rank) == n
+        step_bytes = whole
+    else:
+        assert per_rank == [n, n]
+        step_bytes = 2 * whole
+    assert abs(line["value"] - step_bytes * 3 / (line["ms_per_step"] * 3e-3) / 2 ** 30) <= 0.02 * line["value"] + 0.01
+    # the gathered results on EVERY rank are the oracle's for every rank's packets, in rank order
+    expect = []
+    for rank in (0, 1):
+        if strong:
+            lay = make_layout(config, n=n, shard=(rank, 2))
+        else:
+            lay = make_layout(config, n=n, data_seed=0x5EEDC0DE + 0x1000 * rank)
         arena = splitmix64_bytes(lay.data_seed, lay.arena_bytes)
-        assert np.array_equal(np.array(out, dtype=np.uint16),
-                              oracle.batch(arena, lay.off, lay.length, lay.seed, complement=True))
+        expect.append(oracle.batch(arena, lay.off, lay.length, lay.seed, complement=True))
+    expect = np.concatenate(expect)
+    for rank in (0, 1):
+        assert res[rank]["counts"] == per_rank
+        assert np.array_equal(np.array(res[rank]["gathered"], dtype=np.uint16), expect)

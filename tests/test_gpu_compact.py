@@ -49,8 +49,8 @@ def test_golden_sweep_compact(sweep):
     ln, sd = u32(np.array(sweep["length"])), u16(np.array(sweep["pkt_seed"]))
     expect = np.array(sweep["expect"], dtype=np.uint16)
     for hint in (0, 40, 64, 576, 1500, 9000, 65535):
-        assert np.array_equal(host_u16(csum_batch(arena, off, ln, sd, len_hint=hint)), expect), hint
-        got = csum_batch(arena, off, ln, sd, complement=True, len_hint=hint)
+        assert np.array_equal(host_u16(csum_batch(arena, off, ln, sd, len_hint=hint, compact=True)), expect), hint
+        got = csum_batch(arena, off, ln, sd, complement=True, len_hint=hint, compact=True)
         assert np.array_equal(host_u16(got), expect ^ 0xFFFF), hint
 
 
@@ -74,7 +74,7 @@ def test_random_descriptors_and_bounds(oracle):
     d_off, d_len, d_sd = off32(off), u32(ln), u16(sd)
     for hint in (0, 64, 340, 1500, 9000):
         bad = torch.zeros(1, dtype=torch.int32, device=DEV)
-        got = host_u16(csum_batch(arena, d_off, d_len, d_sd, len_hint=hint, bad=bad))
+        got = host_u16(csum_batch(arena, d_off, d_len, d_sd, len_hint=hint, bad=bad, compact=True))
         assert np.array_equal(got, expect), hint
         assert int(bad.item()) == 100
 
@@ -87,9 +87,22 @@ def test_full_size_compact_equals_64bit(name):
     lay = make_layout(name)
     b = DeviceBatch(lay, DEV)
     ref = csum_batch(b.arena, b.off, b.length, b.seed, complement=True, len_hint=int(lay.mean_len))
-    got = csum_batch(b.arena, off32(lay.off), b.length, b.seed, complement=True, len_hint=int(lay.mean_len))
+    got = csum_batch(b.arena, off32(lay.off), b.length, b.seed, complement=True, len_hint=int(lay.mean_len),
+                     compact=True)
     assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
     if name == "c4_9000B":
         assert int(lay.off.max()) >= 2 ** 31
     del b
     torch.cuda.empty_cache()
+
+
+def test_compact_form_is_explicit():
+    """int32 offsets are the compact form only when asked for: without
+    compact=True they are a TypeError, and compact=True refuses int64 offsets."""
+    arena = torch.zeros(64, dtype=torch.uint8, device=DEV)
+    ln = u32(np.array([8]))
+    with pytest.raises(TypeError):
+        csum_batch(arena, off32(np.array([0])), ln)
+    with pytest.raises(TypeError):
+        csum_batch(arena, torch.zeros(1, dtype=torch.int64, device=DEV), ln, compact=True)
+    assert host_u16(csum_batch(arena, off32(np.array([0])), ln, compact=True))[0] == 0

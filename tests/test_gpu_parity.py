@@ -221,6 +221,32 @@ def test_host_resident_pipeline(oracle, pinned):
         pb.free()
 
 
+def test_host_toolarge_rejected_before_queueing(oracle):
+    """A packet that cannot fit one staging chunk is rejected by the validation
+    pass (RNS_E_TOOLARGE) before any chunk is queued, so no slot is left busy: a
+    second, smaller call on the same context gets exactly its own results and
+    nothing is written past its output (drain skipped on TOOLARGE)."""
+    hb = HostBatcher(device=0, chunk_bytes=4096, nstreams=2)
+    small = 3000
+    ln = np.full(small + 1, 64, dtype=np.uint32)
+    ln[-1] = 9000                                 # c4 jumbo frame: > 4096-byte chunks
+    off = np.zeros(small + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
+    arena = O.splitmix64_bytes(0x7001, int(off[-1]) + 9000)
+    out = np.full(small + 1, 0xABCD, dtype=np.uint16)
+    with pytest.raises(_lib.ChecksumError) as ei:
+        hb.run(arena, off, ln, None, complement=True, out=out)
+    assert ei.value.status == _lib.RNS_E_TOOLARGE
+    assert (out == 0xABCD).all()                 # nothing was queued or drained into it
+    # the next, smaller call on the same context: exact results, no stale slot drained into it
+    n2 = 100
+    guard = np.full(n2 + 64, 0x5A5A, dtype=np.uint16)
+    got = hb.run(arena, off[:n2], ln[:n2], None, complement=True, out=guard[:n2])
+    assert np.array_equal(got, oracle.batch(arena, off[:n2], ln[:n2], None, complement=True))
+    assert (guard[n2:] == 0x5A5A).all()
+    hb.close()
+
+
 def test_arena_beyond_4gib_uses_64bit_path(oracle):
     """Arenas >= 4 GiB cannot use 32-bit buffer offsets: every kernel takes its
     64-bit global-load path.  Packets straddle the 4 GiB line and sit at both ends."""

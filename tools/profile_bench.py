@@ -1,0 +1,87 @@
+"""Reconcile a bench line with the rocprofv3 kernel trace of THE SAME run.
+
+On the GPU box (tools/gpu_session.sh does this):
+
+    rocprofv3 --kernel-trace --stats --output-format csv -d <dir> -o run -- \\
+        python3 bench.py --gpus 1 --steps 20 --warmup 5 > bench.log
+
+then here (or there):
+
+    python tools/profile_bench.py --trace <dir>/run_kernel_trace.csv --bench bench.log \\
+        --out profiles/r02_rocprof_bench_c3_1500B.json
+
+bench.py's own dispatches of the product kernel come first, in order: W warmup
+launches, K timed launches (one event pair around all of them), then, with
+--median-launches M, M launches each inside its own event pair.  Later
+dispatches of the same kernel (the host-pipeline leg's chunks) have smaller
+grids and are excluded by grid size.  Writes the per-dispatch mean and median of
+the K timed launches next to the bench line's kernel_avg_us and the frac each
+implies (and, if present, the event-pair launches' durations).
+"""
+import argparse
+import csv
+import json
+import statistics
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trace", required=True)
+    ap.add_argument("--bench", required=True, help="log holding the bench JSON line")
+    ap.add_argument("--stats", default="", help="run_kernel_stats.csv of the same run (copied into the summary)")
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--kernel", default="csum_", help="substring of the product kernel's name")
+    args = ap.parse_args()
+
+    line = [ln for ln in open(args.bench) if ln.startswith("{")][-1]
+    b = json.loads(line)
+    W, K = b["warmup"], b["steps"]
+    M = b["roofline"].get("evpair_launches", 0)
+    rows = [r for r in csv.DictReader(open(args.trace)) if args.kernel in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    if not rows:
+        raise SystemExit("no dispatch of the product kernel in the trace")
+    grid = int(rows[0]["Grid_Size_X"])
+    name = rows[0]["Kernel_Name"]
+    mine = [r for r in rows if int(r["Grid_Size_X"]) == grid and r["Kernel_Name"] == name]
+    rot = b["config"].get("rotating_batches", 1)
+    need = W + K + M
+    if len(mine) < need:
+        raise SystemExit(f"trace has {len(mine)} dispatches of the bench kernel, expected >= {need}")
+    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in mine[:need]]
+    timed, per = dur[W:W + K], dur[W + K:need]
+    algo = b["roofline"]["algorithmic_bytes_per_launch"]
+    peak = b["roofline"]["peak"]
+
+    def frac(us):
+        return round(algo / (us * 1e-6) / 1e9 / peak, 4)
+
+    gaps = [(int(mine[i + 1]["Start_Timestamp"]) - int(mine[i]["End_Timestamp"])) / 1e3 for i in range(W, W + K - 1)]
+    out = {
+        "command": "rocprofv3 --kernel-trace --stats --output-format csv -- python3 bench.py "
+                   f"--gpus 1 --steps {K} --warmup {W}",
+        "kernel": name,
+        "grid_size_x": grid,
+        "rotating_batches": rot,
+        "dispatches_used": {"warmup": W, "timed": K, "per_launch": M},
+        "rocprof_timed_us": {"mean": round(statistics.mean(timed), 2), "median": round(statistics.median(timed), 2),
+                             "min": round(min(timed), 2), "max": round(max(timed), 2)},
+        "rocprof_evpair_launches_us": ({"mean": round(statistics.mean(per), 2),
+                                        "median": round(statistics.median(per), 2)} if per else None),
+        "rocprof_gap_between_timed_launches_us": {"median": round(statistics.median(gaps), 2) if gaps else None,
+                                                  "max": round(max(gaps), 2) if gaps else None},
+        "bench": {"kernel_avg_us": b["roofline"]["kernel_avg_us"], "evpair_median_us": b["roofline"].get("evpair_median_us"),
+                  "frac": b["roofline"]["frac"], "value": b["value"], "ms_per_step": b["ms_per_step"]},
+        "frac_from_rocprof_timed_median": frac(statistics.median(timed)),
+        "bench_frac_vs_rocprof_timed_median": round(b["roofline"]["frac"] / frac(statistics.median(timed)) - 1, 4),
+    }
+    if args.stats:
+        out["stats_csv"] = [r for r in csv.DictReader(open(args.stats))]
+    with open(args.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps({k: out[k] for k in ("rocprof_timed_us", "rocprof_evpair_launches_us", "bench",
+                                          "frac_from_rocprof_timed_median", "bench_frac_vs_rocprof_timed_median")}))
+
+
+if __name__ == "__main__":
+    main()
