@@ -41,7 +41,7 @@ step bench_prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OU
      python3 "$ROOT/bench.py" --gpus 1 --steps "$STEPS" --warmup "$WARMUP" --config "$CONFIG"
 cd "$ROOT"
 python tools/profile_bench.py --trace "$OUT/prof/run_kernel_trace.csv" --stats "$OUT/prof/run_kernel_stats.csv" \
-     --bench "$OUT/bench_prof.log" --out "$OUT/rocprof_bench_$CONFIG.json" > "$OUT/profile_bench.log" 2>&1
+     --bench "$OUT/bench_prof.log" --out "$OUT/rocprof_bench_$CONFIG.json" --timed-stats-out "$OUT/rocprof_bench_${CONFIG}_timed_stats.csv" > "$OUT/profile_bench.log" 2>&1
 echo "profile_bench rc=$?"; tail -2 "$OUT/profile_bench.log"
 if [ -z "${SKIP_PMC:-}" ]; then
   cd /tmp
