@@ -48,9 +48,11 @@ def parse_args(argv=None):
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="c3_1500B")
-    p.add_argument("--desc", choices=("auto", "64", "32"), default="auto",
-                   help="descriptor offset width: 32 = compact form (rns_csum_batch_dev_off32); "
-                        "auto = 32 when the arena is below 4 GiB")
+    p.add_argument("--desc", choices=("auto", "64", "32", "packed"), default="auto",
+                   help="descriptor form: 64 = u64 offsets (rns_csum_batch_dev); 32 = u32 offsets "
+                        "(rns_csum_batch_dev_off32); packed = u16 lengths + one offset per 64 packets "
+                        "(rns_csum_batch_packed_dev); auto = packed, except for jumbo batches (the group "
+                        "kernel, which has no 64-packet wave batches): 32 below 4 GiB, else 64")
     p.add_argument("--shape", default="", help="variant,G,U,max_blocks kernel shape override (tuning)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample duration (single thread)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -66,7 +68,7 @@ def parse_args(argv=None):
                         "config is one 8M-packet batch over 8 GPUs; weak otherwise)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_{config}.json"))
     args = p.parse_args(argv)
-    if args.shape and args.desc == "32":
+    if args.shape and args.desc in ("32", "packed"):
         p.error("--shape overrides take 64-bit descriptors (--desc 64 or auto)")
     return args
 
@@ -231,11 +233,16 @@ class GpuEngine:
         nrot = max(1, -(-(768 << 20) // max(self.layout.arena_bytes, 1))) if small else 1
         self.batches = [DeviceBatch(self.layout if r == 0 else layout(r), self.device) for r in range(nrot)]
         self.shape = shape
-        if compact == "auto":
-            compact = shape is None and self.layout.arena_bytes + 16 < 2 ** 32
-        self.compact = compact in (True, "32")
-        for b in self.batches:  # bind every rotating batch (and upload compact offsets) before any timing
-            b.launcher(complement=True, shape=shape, compact=self.compact)
+        form = {True: "32", False: "64"}.get(compact, compact)
+        if form == "auto":
+            small = self.layout.arena_bytes + 16 < 2 ** 32
+            jumbo = self.layout.mean_len > 2500  # pick_shape's group kernel: no wave batches, no packed form
+            form = "64" if shape is not None else ("packed" if not jumbo else ("32" if small else "64"))
+        self.form = form
+        self.compact = form == "32"
+        self.packed = form == "packed"
+        for b in self.batches:  # bind every rotating batch (and upload its descriptors) before any timing
+            b.launcher(complement=True, shape=shape, compact=self.compact, packed=self.packed)
         self.k = 0
         self.last = self.batches[0]
         self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -254,7 +261,7 @@ class GpuEngine:
     def step(self):
         b = self.batches[self.k % len(self.batches)]
         self.k += 1
-        b.launcher(complement=True, shape=self.shape, compact=self.compact)()  # pre-bound: one ctypes call
+        b.launcher(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)()  # one ctypes call
         self.last = b
 
     def gather(self):
@@ -454,7 +461,9 @@ def main(argv=None):
     kernel_ms = r["kernel_ms"]
     per = engine.per_launch_us(args.median_launches) if args.median_launches > 0 else []
     algo_bytes = engine.payload_bytes + 2 * engine.n
-    desc_bytes = engine.n * ((4 if engine.compact else 8) + 4 + 2)
+    # descriptor bytes a launch reads (seeds included): packed 2 B length + 8 B per 64 packets
+    desc_bytes = (engine.n * (2 + 2) + 8 * ((engine.n + 63) // 64) if engine.packed
+                  else engine.n * ((4 if engine.compact else 8) + 4 + 2))
     kernel_us = kernel_ms * 1e3
     achieved = algo_bytes / (kernel_us * 1e-6) / 1e9
     traffic = load_traffic(args.traffic_json, args.config)
@@ -479,8 +488,10 @@ def main(argv=None):
             "batch": "one batch sharded by packet index across ranks" if strong else "a full batch per rank",
             "parallelism": f"packet shards x{dist.world}, no data-path collective in `value`",
             "kernel_shape": list(shape) if shape else "auto",
-            "descriptors": ("u32 offset + u32 length + u16 seed (rns_csum_batch_dev_off32)" if engine.compact
-                            else "u64 offset + u32 length + u16 seed (rns_csum_batch_dev)"),
+            "descriptors": {"32": "u32 offset + u32 length + u16 seed (rns_csum_batch_dev_off32)",
+                            "64": "u64 offset + u32 length + u16 seed (rns_csum_batch_dev)",
+                            "packed": "packed: u16 length + u16 seed per packet, u64 offset per 64 packets "
+                                      "(rns_csum_batch_packed_dev)"}[engine.form],
             "rotating_batches": len(engine.batches),
         },
         "roofline": {

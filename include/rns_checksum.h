@@ -117,6 +117,25 @@ int rns_csum_batch_dev_off32(const uint8_t *d_arena, uint64_t arena_bytes, const
                              const uint32_t *d_len, const uint16_t *d_seed, uint16_t *d_out, uint32_t n,
                              uint32_t flags, uint32_t len_hint, uint32_t *d_bad, void *stream);
 
+/* Packed descriptors: packets lie back to back in index order, packet i+1
+ * starting at the first multiple of 2^align_log2 at or after the end of packet i
+ * (align_log2 <= 12), as a batched receive packs datagrams into one arena.  Only
+ * the lengths travel (d_len16: u16 per packet — an IP datagram's length field is
+ * 16 bits) plus d_blk_off[b] = the offset of packet 64*b, one u64 per 64 packets
+ * (rns_packed_layout computes them): 2.1 B of descriptors per packet instead of
+ * 10 (off32) or 14.  Per packet exactly util.rs:88-110, as rns_csum_batch_dev;
+ * a packet outside the arena gets 0 and is counted in *d_bad. */
+int rns_csum_batch_packed_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_blk_off,
+                              const uint16_t *d_len16, uint32_t align_log2, const uint16_t *d_seed, uint16_t *d_out,
+                              uint32_t n, uint32_t flags, uint32_t len_hint, uint32_t *d_bad, void *stream);
+
+/* Host helper for the packed form: given the n lengths, the alignment and the
+ * first packet's offset, writes the (n + 63) / 64 block offsets to blk_off and
+ * the offset just past the last packet's padded end to *end (the arena size the
+ * packing needs).  Optionally (off != NULL) every packet's offset.  CPU only. */
+int rns_packed_layout(const uint16_t *len16, uint64_t n, uint32_t align_log2, uint64_t first_off, uint64_t *blk_off,
+                      uint64_t *off, uint64_t *end);
+
 /* Same, for packets at a fixed stride (no offset/length arrays to read):
  * packet i = d_arena[first_off + i*stride .. + len). */
 int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uint64_t first_off,
@@ -126,12 +145,15 @@ int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uin
 /* Fragment chains: util.rs:112 `compute_buffer_ones_comp` for a batch of
  * NetBuffer-style fragment lists (buf.rs:466-487).  Packet i is fragments
  * [d_first[i], d_first[i+1]) of (d_frag_off, d_frag_len) — d_first has n_pkts+1
- * entries; each fragment is folded on its own, so an odd-length non-final
- * fragment is zero-padded exactly like the per-fragment call.  d_frag_sums is
- * device scratch of n_frags u16 (receives compute_ones_comp(0, fragment)).
- * A packet with a fragment outside the arena gets 0 and is counted in *d_bad.
- * Exact for fragments up to 128 KiB (NetBuffer fragments are 512 B, buf.rs:50);
- * an empty fragment contributes nothing (the reference panics on it). */
+ * entries; each fragment is folded on its own and the running sum is folded after
+ * every fragment, exactly as the reference's loop: an odd-length non-final
+ * fragment is zero-padded like the per-fragment call, and the result is exact for
+ * ANY fragment count and fragment size (a fragment past 128 KiB wraps the u32
+ * accumulator from the running sum, as util.rs:89-99 does in a release build).
+ * One pass, one kernel; d_frag_sums is unused (the round-1 two-pass scratch; may
+ * be NULL).  A packet whose range is malformed (end < start, end > n_frags) or
+ * that has a fragment outside the arena gets 0 and is counted in *d_bad.  An empty
+ * fragment contributes nothing (the reference panics on it). */
 int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_frag_off,
                        const uint32_t *d_frag_len, uint32_t n_frags, const uint32_t *d_first,
                        const uint16_t *d_seed, uint16_t *d_out, uint32_t n_pkts, uint32_t flags,
@@ -194,6 +216,8 @@ int rns_tx_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_of
  * loads; bit 2: mixed kernel (rounds kernel that sorts each wave's 64 packets
  * into size classes, each with its own shape; G and U are ignored); bit 3 (with
  * bit 0 only): rounds kernel with every round of a batch in flight (G <= 8, U <= 2);
+ * bit 4 (with bit 0 only, not with bit 3): rounds kernel that loads the next wave
+ * batch's descriptors before the current batch's data (G <= 8, U <= 2);
  * bits 8-11: at most that many 4-wave workgroups per CU (an occupancy cap, by LDS
  * reservation; 0 = none).
  * lanes_per_packet in {4,8,16,32,64} (2 too for the rounds kernel); unroll (16-byte

@@ -44,6 +44,8 @@ EXPORTED_SYMBOLS = (
     "rns_compute_pseudo_header_checksum",
     "rns_csum_batch_dev",
     "rns_csum_batch_dev_off32",
+    "rns_csum_batch_packed_dev",
+    "rns_packed_layout",
     "rns_csum_batch_strided_dev",
     "rns_csum_batch_dev_cfg",
     "rns_csum_chain_dev",
@@ -112,6 +114,8 @@ _SIGNATURES = {
     "rns_compute_pseudo_header_checksum": (_i32, [ctypes.POINTER(RnsIpAddr), ctypes.POINTER(RnsIpAddr), _u64, _u8]),
     "rns_csum_batch_dev": (_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp]),
     "rns_csum_batch_dev_off32": (_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp]),
+    "rns_csum_batch_packed_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp, _u32, _u32, _u32, _vp, _vp]),
+    "rns_packed_layout": (_int, [_vp, _u64, _u32, _u64, _vp, _vp, ctypes.POINTER(_u64)]),
     "rns_csum_batch_strided_dev": (_int, [_vp, _u64, _u64, _u64, _u32, _vp, _vp, _u32, _u32, _vp, _vp]),
     "rns_csum_batch_dev_cfg": (_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _u32, _vp, _vp]),
     "rns_csum_chain_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp]),

@@ -124,6 +124,93 @@ class PreparedBatch:
         return self.out
 
 
+def packed_layout(length, align_log2: int = 4, first_off: int = 0):
+    """Offsets of the packed form (rns_packed_layout): packets back to back in index
+    order, each starting at the next multiple of 2**align_log2.  ``length``: lengths
+    (< 65536).  Returns (blk_off uint64 [ceil(n/64)], off uint64 [n], end)."""
+    import numpy as np
+    ln = np.asarray(length)
+    if ln.size and (int(ln.max()) > 0xFFFF or int(ln.min()) < 0):
+        raise ValueError("packed descriptors hold u16 lengths (< 65536)")
+    len16 = np.ascontiguousarray(ln, dtype=np.uint16)
+    n = int(len16.size)
+    blk = np.zeros(max((n + 63) // 64, 1), dtype=np.uint64)
+    off = np.zeros(max(n, 1), dtype=np.uint64)
+    end = ctypes.c_uint64(0)
+    st = _lib.load().rns_packed_layout(len16.ctypes.data, n, int(align_log2), int(first_off), blk.ctypes.data,
+                                       off.ctypes.data, ctypes.byref(end))
+    _lib.check(st, "rns_packed_layout")
+    return blk[:(n + 63) // 64], off[:n], int(end.value)
+
+
+class PackedBatch:
+    """A device-resident batch in the packed form (rns_csum_batch_packed_dev), bound
+    once like PreparedBatch: ``blk_off`` int64 [ceil(n/64)] (the offset of every 64th
+    packet), ``len16`` int16/uint16 [n] (lengths as unsigned 16-bit), packets back to
+    back at 2**align_log2 boundaries (see packed_layout)."""
+
+    def __init__(self, arena: torch.Tensor, blk_off: torch.Tensor, len16: torch.Tensor,
+                 seed: torch.Tensor | None = None, *, align_log2: int = 4, complement: bool = False,
+                 out: torch.Tensor | None = None, len_hint: int = 0, bad: torch.Tensor | None = None):
+        _require_cuda(arena, "arena", (torch.uint8,))
+        _require_cuda(blk_off, "blk_off", (torch.int64,))
+        _require_cuda(len16, "len16", _U16)
+        n = len16.numel()
+        if blk_off.numel() != (n + 63) // 64:
+            raise ValueError("blk_off must have one entry per 64 packets")
+        if not 0 <= align_log2 <= 12:
+            raise ValueError("align_log2 must be in 0..12")
+        dev = arena.device
+        for name, t in (("blk_off", blk_off), ("len16", len16)):
+            if t.device != dev:
+                raise ValueError(f"{name} is on {t.device}, arena on {dev}")
+        seed_ptr = None
+        if seed is not None:
+            _require_cuda(seed, "seed", _U16)
+            if seed.numel() != n or seed.device != dev:
+                raise ValueError("seed must have one entry per packet on the arena's device")
+            seed_ptr = seed.data_ptr()
+        if out is None:
+            out = torch.empty(n, dtype=torch.uint16, device=dev)
+        else:
+            _require_cuda(out, "out", _U16)
+            if out.numel() != n or out.device != dev:
+                raise ValueError("out must have one entry per packet on the arena's device")
+        bad_ptr = None
+        if bad is not None:
+            _require_cuda(bad, "bad", (torch.int32,))
+            bad_ptr = bad.data_ptr()
+        lib = _lib.load()
+        self._keep = (arena, blk_off, len16, seed, out, bad)
+        self.out, self.n, self.device = out, n, dev
+        self._fn = lib.rns_csum_batch_packed_dev
+        self._args = (arena.data_ptr(), arena.numel(), blk_off.data_ptr(), len16.data_ptr(), int(align_log2),
+                      seed_ptr, out.data_ptr(), n, _lib.RNS_FLAG_COMPLEMENT if complement else 0, int(len_hint),
+                      bad_ptr, _stream_handle(dev))
+
+    def __call__(self) -> torch.Tensor:
+        if self.n:
+            if torch.cuda.current_device() != self.device.index:
+                with torch.cuda.device(self.device):
+                    st = self._fn(*self._args)
+            else:
+                st = self._fn(*self._args)
+            if st != _lib.RNS_OK:
+                raise _lib.ChecksumError(st, "rns_csum_batch_packed_dev")
+        return self.out
+
+
+def csum_batch_packed(arena: torch.Tensor, blk_off: torch.Tensor, len16: torch.Tensor,
+                      seed: torch.Tensor | None = None, *, align_log2: int = 4, complement: bool = False,
+                      out: torch.Tensor | None = None, len_hint: int = 0,
+                      bad: torch.Tensor | None = None) -> torch.Tensor:
+    """Checksum a batch in the packed form (offsets implied by lengths; see PackedBatch)."""
+    _require_cuda(arena, "arena", (torch.uint8,))
+    with torch.cuda.device(arena.device):
+        return PackedBatch(arena, blk_off, len16, seed, align_log2=align_log2, complement=complement, out=out,
+                           len_hint=len_hint, bad=bad)()
+
+
 def csum_batch(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, seed: torch.Tensor | None = None,
                *, complement: bool = False, out: torch.Tensor | None = None, len_hint: int = 0,
                bad: torch.Tensor | None = None, shape: tuple[int, int, int, int] | None = None,
@@ -173,7 +260,8 @@ def csum_chain(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch.Tens
     """util.rs:112 ``compute_buffer_ones_comp`` for a batch of fragment chains.
 
     Packet i = fragments ``first[i] .. first[i+1]`` (``first``: int32 [n+1]) of
-    ``(frag_off, frag_len)``; each fragment is folded on its own like the reference.
+    ``(frag_off, frag_len)``; each fragment is folded on its own like the reference,
+    in one pass (``frag_sums`` is accepted for compatibility and unused).
     """
     _require_cuda(arena, "arena", (torch.uint8,))
     _require_cuda(frag_off, "frag_off", (torch.int64,))
@@ -192,15 +280,14 @@ def csum_chain(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch.Tens
         seed_ptr = seed.data_ptr()
     if out is None:
         out = torch.empty(max(n, 0), dtype=torch.uint16, device=dev)
-    if frag_sums is None:
-        frag_sums = torch.empty(max(nf, 1), dtype=torch.uint16, device=dev)
     bad_ptr = bad.data_ptr() if bad is not None else None
     lib = _lib.load()
     with torch.cuda.device(dev):
         st = lib.rns_csum_chain_dev(arena.data_ptr(), arena.numel(), frag_off.data_ptr(), frag_len.data_ptr(), nf,
                                     first.data_ptr(), seed_ptr, out.data_ptr(), n,
                                     _lib.RNS_FLAG_COMPLEMENT if complement else 0, frag_len_hint,
-                                    frag_sums.data_ptr(), bad_ptr, _stream_handle(dev))
+                                    frag_sums.data_ptr() if frag_sums is not None else None, bad_ptr,
+                                    _stream_handle(dev))
     _lib.check(st, "rns_csum_chain_dev")
     return out
 

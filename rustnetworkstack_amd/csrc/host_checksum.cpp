@@ -130,6 +130,24 @@ int32_t rns_compute_pseudo_header_checksum(const rns_ipaddr *source_ip, const rn
     return ones_comp(0, ph, 40);
 }
 
+int rns_packed_layout(const uint16_t *len16, uint64_t n, uint32_t align_log2, uint64_t first_off, uint64_t *blk_off,
+                      uint64_t *off, uint64_t *end)
+{
+    if ((n && (!len16 || !blk_off)) || !end || align_log2 > 12)
+        return RNS_E_INVALID;
+    const uint64_t m = (1ull << align_log2) - 1;
+    uint64_t at = first_off;
+    for (uint64_t i = 0; i < n; ++i) {
+        if ((i & 63) == 0)
+            blk_off[i >> 6] = at;
+        if (off)
+            off[i] = at;
+        at += (static_cast<uint64_t>(len16[i]) + m) & ~m;  // the kernels' padded length
+    }
+    *end = at;
+    return RNS_OK;
+}
+
 int rns_abi_version(void) { return RNS_ABI_VERSION; }
 
 const char *rns_strerror(int status)

@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -65,6 +66,12 @@ struct CsumArgs {
     uint16_t *l4_out;          // receive verify: complemented L4 sum (optional)
     uint32_t local4_sum;       // receive verify: BE word sums of the local addresses
     uint32_t local6_sum;
+    const uint16_t *len16;     // packed form: u16 lengths, offsets implied (used when non-null)
+    const uint64_t *blk_off;   // packed form: offset of packet 64*b, per block b of 64 packets
+    uint32_t align_mask;       // packed form: packet starts are multiples of align_mask + 1
+    const uint32_t *first;     // fragment chains: packet i = fragments [first[i], first[i+1]) (off/len = fragments)
+    uint32_t n_frags;
+    uint32_t chain_k;          // fragment chains: packets per lane (a wave owns 64*chain_k consecutive packets)
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -75,6 +82,43 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint64_t desc_off(const CsumArgs &a, uint64_t p)
 {
     return a.off32 ? static_cast<uint64_t>(a.off32[p]) : a.off[p];
+}
+
+// Packed form (rns_csum_batch_packed_dev): packets lie back to back in index order,
+// each starting at the next multiple of (align_mask + 1) after the previous one's
+// end, so a packet's offset is its 64-packet block's base plus the padded lengths
+// of the packets before it in the block — an exclusive scan across the wave that
+// owns the block (every lane calls this with p = base + lane, base a multiple of
+// 64).  Descriptors: 2 B of length per packet + 8 B per 64 packets.
+template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF>
+__device__ __forceinline__ uint32_t dpp_or_zero(uint32_t v)
+{
+    // lanes the masks disable, and lanes whose source lies outside the row, read 0
+    return static_cast<uint32_t>(
+        __builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, ROW_MASK, BANK_MASK, true));
+}
+
+// Exclusive prefix sum of the lanes' padded lengths: the classic gfx9 DPP scan
+// (row_shr 1,2,3 / 4 / 8 within each row of 16, then row_bcast:15 and row_bcast:31
+// across rows) — VALU only, no LDS round trip.
+__device__ __forceinline__ uint32_t packed_scan(const CsumArgs &a, uint32_t lane, uint32_t len)
+{
+    (void)lane;
+    const uint32_t pad = (len + a.align_mask) & ~a.align_mask;  // < 2^17: the block's sum fits 32 bits
+    uint32_t x = pad;
+    x += dpp_or_zero<0x111>(pad);            // row_shr:1
+    x += dpp_or_zero<0x112>(pad);            // row_shr:2
+    x += dpp_or_zero<0x113>(pad);            // row_shr:3
+    x += dpp_or_zero<0x114, 0xF, 0xE>(x);    // row_shr:4, banks 1-3
+    x += dpp_or_zero<0x118, 0xF, 0xC>(x);    // row_shr:8, banks 2-3
+    x += dpp_or_zero<0x142, 0xA, 0xF>(x);    // row_bcast:15 into rows 1 and 3
+    x += dpp_or_zero<0x143, 0xC, 0xF>(x);    // row_bcast:31 into rows 2 and 3
+    return x - pad;
+}
+
+__device__ __forceinline__ uint64_t packed_off(const CsumArgs &a, uint64_t base, uint32_t lane, uint32_t len)
+{
+    return a.blk_off[base >> 6] + packed_scan(a, lane, len);
 }
 
 // Cache-policy bits of the "nontemporal" buffer loads (gfx950 CPol: 1 = sc0, 2 = nt,
@@ -519,7 +563,10 @@ __device__ __forceinline__ uint16_t finalize(uint32_t mine, uint64_t d_start, ui
 // D = rounds in flight: 1 = the next round's first pass is issued before the current
 // round is consumed; D = G (small G only) = all rounds of the batch are issued up
 // front, so a batch of tiny packets costs one memory latency instead of G.
-template <int G, int U, bool STRIDED, bool NT, bool BUF, int D = 1>
+// PF: the next wave batch's descriptors are loaded (branch-free) before the current
+// batch's data, so a wave's descriptor latency overlaps its previous batch instead of
+// preceding each batch's first data load (tiny packets: a batch is only G rounds).
+template <int G, int U, bool STRIDED, bool NT, bool BUF, int D = 1, bool PACKED = false, bool PF = false>
 __global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
 {
     static_assert(G >= 2 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two in [2,64]");
@@ -534,20 +581,59 @@ __global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
 
-    for (uint64_t base = static_cast<uint64_t>(wave) * 64; base < a.n; base += static_cast<uint64_t>(nwaves) * 64) {
+    const uint64_t wstride = static_cast<uint64_t>(nwaves) * 64;
+    // PF: raw descriptors of the batch at `base` (packed: the length and the block base)
+    uint64_t r_off = 0;
+    uint32_t r_len = 0, r_seed = 0;
+    auto fetch_raw = [&](uint64_t b) {
+        const uint64_t q = b + lane < a.n ? b + lane : a.n - 1;  // branch-free: past the end re-reads the last
+        if constexpr (PACKED) {
+            r_len = a.len16[q];
+            r_off = a.blk_off[(b < a.n ? b : a.n - 1) >> 6];
+        } else if constexpr (!STRIDED) {
+            r_off = desc_off(a, q);
+            r_len = a.len[q];
+        }
+        r_seed = a.seed ? a.seed[q] : 0u;
+    };
+    if constexpr (PF)
+        fetch_raw(static_cast<uint64_t>(wave) * 64);
+
+    for (uint64_t base = static_cast<uint64_t>(wave) * 64; base < a.n; base += wstride) {
         const uint64_t p = base + lane;
         const bool live = p < a.n;
         uint64_t d_start = 0;
         uint32_t d_len = 0, d_seed = 0;
-        if (live) {
+        if constexpr (PF) {
+            const uint64_t c_off = r_off;
+            const uint32_t c_len = r_len, c_seed = r_seed;
+            fetch_raw(base + wstride);  // the next batch's descriptors, in flight during this one
+            d_seed = live ? c_seed : 0u;
             if constexpr (STRIDED) {
                 d_start = a.first_off + p * a.stride;
-                d_len = a.fixed_len;
+                d_len = live ? a.fixed_len : 0u;
+            } else if constexpr (PACKED) {
+                d_len = live ? c_len : 0u;
+                d_start = c_off + packed_scan(a, lane, d_len);
             } else {
-                d_start = desc_off(a, p);
-                d_len = a.len[p];
+                d_start = live ? c_off : 0;
+                d_len = live ? c_len : 0u;
             }
-            d_seed = a.seed ? a.seed[p] : 0u;
+        } else {
+            if (live) {
+                if constexpr (STRIDED) {
+                    d_start = a.first_off + p * a.stride;
+                    d_len = a.fixed_len;
+                } else if constexpr (!PACKED) {
+                    d_start = desc_off(a, p);
+                    d_len = a.len[p];
+                }
+                d_seed = a.seed ? a.seed[p] : 0u;
+            }
+            if constexpr (PACKED) {  // lengths only, offsets from the wave's scan
+                d_len = live ? a.len16[p] : 0u;
+                d_start = packed_off(a, base, lane, d_len);
+            }
         }
         d_start += a.base_adjust;
         const bool d_ok = d_start <= a.arena_bytes && d_len <= a.arena_bytes - d_start;
@@ -741,6 +827,73 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
         v[u] = w[u];
 }
 
+// The size-class data pass over one wave batch: lane l holds one descriptor
+// (d_start, d_len; d_aux = the field offset for kStashField; d_len 0 = nothing to
+// read) and receives that packet's word sum — the LE sum for packets <= 128 KiB,
+// the exact BE sum mod 2^32 above.  The wave sorts its 64 descriptors by size class
+// (ballot + mbcnt ranks, ds_permute), runs every class's rounds with its own shape,
+// and routes each sum back to its owner lane.  pos = the lane's sorted position
+// (its stash slot).
+template <bool NT, bool BUF, int MODE>
+__device__ __forceinline__ uint32_t wave_class_pass(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint64_t d_start,
+                                                    uint32_t d_len, uint32_t d_aux, uint32_t lane, uint4 *st,
+                                                    uint32_t &pos)
+{
+    // size class of this lane's packet; ranks within the class; sorted position
+    const uint32_t nch = d_len ? static_cast<uint32_t>(((d_start & 15) + d_len + 15) >> 4) : 0u;
+    uint32_t cls = kNumClasses - 1;
+#pragma unroll
+    for (int c = kNumClasses - 2; c >= 0; --c)
+        cls = (nch <= kClassMax[c]) ? static_cast<uint32_t>(c) : cls;
+    uint32_t rank = 0, off = 0;
+    pos = 0;
+    ClassRun cr[kNumClasses];
+#pragma unroll
+    for (uint32_t c = 0; c < kNumClasses; ++c) {
+        const uint64_t m = __ballot(cls == c);
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+        if (cls == c) {
+            rank = below;
+            pos = off + below;
+        }
+        cr[c] = ClassRun{off, static_cast<uint32_t>(__popcll(m))};
+        off += cr[c].cnt;
+    }
+    // next non-empty class after each class (wave-uniform); kNumClasses = none
+    uint32_t next[kNumClasses + 1];
+    next[kNumClasses] = kNumClasses;
+#pragma unroll
+    for (int c = kNumClasses - 1; c >= 0; --c)
+        next[c] = cr[c].cnt ? static_cast<uint32_t>(c) : next[c + 1];
+    // sort the descriptors by class: lane `pos` receives this lane's packet
+    const int addr = static_cast<int>(pos * 4);
+    const uint32_t s_lo = static_cast<uint32_t>(
+        __builtin_amdgcn_ds_permute(addr, static_cast<int>(static_cast<uint32_t>(d_start))));
+    const uint32_t s_hi = static_cast<uint32_t>(
+        __builtin_amdgcn_ds_permute(addr, static_cast<int>(static_cast<uint32_t>(d_start >> 32))));
+    const uint32_t s_len = static_cast<uint32_t>(__builtin_amdgcn_ds_permute(addr, static_cast<int>(d_len)));
+    const uint64_t s_start = (static_cast<uint64_t>(s_hi) << 32) | s_lo;
+    const uint32_t s_aux = MODE == kStashField
+        ? static_cast<uint32_t>(__builtin_amdgcn_ds_permute(addr, static_cast<int>(d_aux))) : 0u;
+
+    uint32_t mine = 0;
+    uint4 v[kUMax];
+    Pkt cur = prefetch_class<NT, BUF, MODE>(a, rsrc, next[0], cr, s_start, s_len, s_aux, lane, v);
+#define RNS_RUN_CLASS(C)                                                                                  \
+    run_class<C, NT, BUF, MODE>(a, rsrc, cr, next[C + 1], s_start, s_len, s_aux, cls == C, rank, lane, \
+                                cur, v, mine, st)
+    RNS_RUN_CLASS(0);
+    RNS_RUN_CLASS(1);
+    RNS_RUN_CLASS(2);
+    RNS_RUN_CLASS(3);
+    RNS_RUN_CLASS(4);
+    if constexpr (kNumClasses > 5)
+        RNS_RUN_CLASS(5 % kNumClasses);
+#undef RNS_RUN_CLASS
+    return mine;
+}
+
 // ---------------------------------------------------------------------------
 // Receive verify (§8f row 1), fused into the mixed kernel (kStashHead): the checks
 // ip_input_v4 (ip.rs:65-92), ip_input_v6 (ip.rs:108-115), ip_input_common
@@ -907,7 +1060,7 @@ struct Desc {
     uint32_t len, field;
 };
 
-template <bool STRIDED, bool FILL, bool BUF>
+template <bool STRIDED, bool FILL, bool BUF, bool PACKED = false>
 __device__ __forceinline__ Desc<BUF> load_desc(const CsumArgs &a, uint64_t p)
 {
     const bool live = p < a.n;
@@ -917,6 +1070,9 @@ __device__ __forceinline__ Desc<BUF> load_desc(const CsumArgs &a, uint64_t p)
     if constexpr (STRIDED) {
         off = a.first_off + q * a.stride;
         d.len = a.fixed_len;
+    } else if constexpr (PACKED) {  // lengths only, offsets from the wave's scan
+        d.len = live ? a.len16[q] : 0u;
+        off = packed_off(a, p & ~63ull, static_cast<uint32_t>(p & 63), d.len);
     } else {
         off = desc_off(a, q);
         d.len = a.len[q];
@@ -945,7 +1101,7 @@ constexpr int kMixedBlock = STASH ? 64 : kBlock;
 // folds, and stores the (complemented) result into the field big-endian (set_be16,
 // util.rs:132-135) after the whole wave has read its 64 packets.
 // RX: receive verify (see above).
-template <bool STRIDED, bool NT, bool BUF, bool FILL, bool RX = false, bool TX = false>
+template <bool STRIDED, bool NT, bool BUF, bool FILL, bool RX = false, bool TX = false, bool PACKED = false>
 #ifndef RNS_MIXED_OCC
 #define RNS_MIXED_OCC 4
 #endif
@@ -972,11 +1128,12 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX
     for (uint64_t base = static_cast<uint64_t>(wave) * kPer; base < a.n; base += wstep) {
         const uint64_t p = base + lane;
         const bool live = p < a.n;
-        const Desc<BUF> cd = load_desc<STRIDED, FILL, BUF>(a, p);
+        const Desc<BUF> cd = load_desc<STRIDED, FILL, BUF, PACKED>(a, p);
         uint64_t d_start = cd.off + a.base_adjust;
         // the seed is first needed after the data pass: loaded here, its latency is hidden
         uint32_t d_len = cd.len;
-        const uint32_t d_seed = (a.seed && live) ? a.seed[p] : 0u;
+        // (packed form: loaded after the class pass — held across it, the seed spilled to scratch)
+        uint32_t d_seed = (!PACKED && a.seed && live) ? a.seed[p] : 0u;
         const uint32_t d_field = cd.field;  // FILL: the field offset
         bool d_ok = d_start <= a.arena_bytes && d_len <= a.arena_bytes - d_start;
         if constexpr (FILL) {
@@ -989,57 +1146,8 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX
             d_start = 0;
         }
         const bool odd = d_start & 1, big = d_len > kNoWrapBytes;  // all finalize needs of (start, len)
-        // size class of this lane's packet; ranks within the class; sorted position
-        const uint32_t nch = d_len ? static_cast<uint32_t>(((d_start & 15) + d_len + 15) >> 4) : 0u;
-        uint32_t cls = kNumClasses - 1;
-#pragma unroll
-        for (int c = kNumClasses - 2; c >= 0; --c)
-            cls = (nch <= kClassMax[c]) ? static_cast<uint32_t>(c) : cls;
-        uint32_t pos = 0, rank = 0, off = 0;
-        ClassRun cr[kNumClasses];
-#pragma unroll
-        for (uint32_t c = 0; c < kNumClasses; ++c) {
-            const uint64_t m = __ballot(cls == c);
-            const uint32_t below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
-            if (cls == c) {
-                rank = below;
-                pos = off + below;
-            }
-            cr[c] = ClassRun{off, static_cast<uint32_t>(__popcll(m))};
-            off += cr[c].cnt;
-        }
-        // next non-empty class after each class (wave-uniform); kNumClasses = none
-        uint32_t next[kNumClasses + 1];
-        next[kNumClasses] = kNumClasses;
-#pragma unroll
-        for (int c = kNumClasses - 1; c >= 0; --c)
-            next[c] = cr[c].cnt ? static_cast<uint32_t>(c) : next[c + 1];
-        // sort the descriptors by class: lane `pos` receives this lane's packet
-        const int addr = static_cast<int>(pos * 4);
-        const uint32_t s_lo = static_cast<uint32_t>(
-            __builtin_amdgcn_ds_permute(addr, static_cast<int>(static_cast<uint32_t>(d_start))));
-        const uint32_t s_hi = static_cast<uint32_t>(
-            __builtin_amdgcn_ds_permute(addr, static_cast<int>(static_cast<uint32_t>(d_start >> 32))));
-        const uint32_t s_len = static_cast<uint32_t>(__builtin_amdgcn_ds_permute(addr, static_cast<int>(d_len)));
-        const uint64_t s_start = (static_cast<uint64_t>(s_hi) << 32) | s_lo;
-        const uint32_t s_aux = FILL
-            ? static_cast<uint32_t>(__builtin_amdgcn_ds_permute(addr, static_cast<int>(d_field))) : 0u;
-
-        uint32_t mine = 0;
-        uint4 v[kUMax];
-        Pkt cur = prefetch_class<NT, BUF, kMode>(a, rsrc, next[0], cr, s_start, s_len, s_aux, lane, v);
-#define RNS_RUN_CLASS(C)                                                                                   \
-        run_class<C, NT, BUF, kMode>(a, rsrc, cr, next[C + 1], s_start, s_len, s_aux, cls == C, rank, lane, \
-                                     cur, v, mine, st)
-        RNS_RUN_CLASS(0);
-        RNS_RUN_CLASS(1);
-        RNS_RUN_CLASS(2);
-        RNS_RUN_CLASS(3);
-        RNS_RUN_CLASS(4);
-        if constexpr (kNumClasses > 5)
-            RNS_RUN_CLASS(5 % kNumClasses);
-#undef RNS_RUN_CLASS
+        uint32_t pos;
+        uint32_t mine = wave_class_pass<NT, BUF, kMode>(a, rsrc, d_start, d_len, d_field, lane, st, pos);
 
         if constexpr (TX) {
             // Transmit finalize: mine = the whole datagram's word sum.  From the stash
@@ -1216,6 +1324,8 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX
                 w_size = in ? bs : w_size;
             }
         }
+        if constexpr (PACKED)
+            d_seed = (a.seed && live) ? a.seed[p] : 0u;
         const uint16_t res = finalize_bits(mine, odd, big, d_seed, d_ok, a.flags);
         if (live && a.out)
             a.out[p] = res;  // 64 consecutive u16: one 128-byte store
@@ -1264,43 +1374,143 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX
 
 // ---------------------------------------------------------------------------
 // Fragment chains (util.rs:112-119 compute_buffer_ones_comp over NetBuffer
-// fragments, buf.rs:466-487).  Pass 1 is the packet kernel run over FRAGMENTS
-// with seed 0: frag_sums[f] = compute_ones_comp(0, fragment f), pairing bytes from
-// the fragment's own start exactly as the per-fragment call does.  Pass 2 (this
-// kernel) chains them: for fragments <= 128 KiB no step can wrap the u32, so the
-// reference's fold-after-every-fragment equals ONE end-around fold of
-// seed + sum(frag_sums) — both are the unique value in [1, 0xffff] congruent mod
-// 0xffff to seed + all words, or 0 when seed and every byte are 0.
+// fragments, buf.rs:466-487), in ONE pass.  A wave owns 64 consecutive packets;
+// their fragments [F0, F1) (CSR `first`) stream through the size-class pass 64 at
+// a time, each fragment paired from its own start exactly as the per-fragment call
+// pairs it.  Each owner lane then applies the reference's step to its own
+// fragments, in order, fetching their sums from the lanes that computed them:
+//   fragment <= 128 KiB: sum = fold(sum + fold(W)).  No u32 wrap is possible, so
+//     this is util.rs:89-103 with in_checksum = sum (same residue mod 0xffff, zero
+//     iff both are zero);
+//   longer: sum = fold((sum + W) mod 2^32), W = the exact BE word sum mod 2^32 —
+//     the reference's wrapping u32 accumulator itself.
+// Exact for any fragment count and size; no scratch, no second kernel.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void chain_combine_kernel(const uint64_t *__restrict__ frag_off,
-                                                               const uint32_t *__restrict__ frag_len,
-                                                               const uint16_t *__restrict__ frag_sums,
-                                                               uint32_t n_frags, const uint32_t *__restrict__ first,
-                                                               const uint16_t *__restrict__ seed,
-                                                               uint16_t *__restrict__ out, uint32_t n_pkts,
-                                                               uint64_t arena_bytes, uint32_t flags, uint32_t *bad)
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
 {
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_pkts; i += stride) {
-        const uint32_t f0 = first[i], f1 = first[i + 1];
-        bool ok = f0 <= f1 && f1 <= n_frags;
-        uint32_t acc = seed ? seed[i] : 0u;
-        for (uint32_t f = f0; ok && f < f1; ++f) {
-            const uint64_t o = frag_off[f];
-            const uint32_t L = frag_len[f];
-            ok = o <= arena_bytes && L <= arena_bytes - o;
-            acc += frag_sums[f];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1)
+        v = min(v, static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), m, 64)));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1)
+        v = max(v, static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), m, 64)));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+constexpr uint32_t kChainMaxK = 8;  // packets per lane, at most
+
+template <bool NT, bool BUF, uint32_t KMAX>
+__global__ __launch_bounds__(kBlock, 4) void csum_chain_kernel(const CsumArgs a)
+{
+    // A wave owns K*64 consecutive packets (K = a.chain_k, chosen by the host from the
+    // mean fragment count so the wave's fragments fill whole 64-fragment batches).
+    // Per-packet state is parked in LDS across the class pass (which needs every VGPR
+    // of a 4-waves/SIMD budget): the fragment range and the running sum (bit 31 = a
+    // bad descriptor seen).
+    __shared__ uint32_t pk_lds[kBlock / 64][3][KMAX * 64];
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t (&pk)[3][KMAX * 64] = pk_lds[threadIdx.x >> 6];
+    const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
+    const uint32_t K = KMAX == 1 ? 1u : a.chain_k;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
+    constexpr uint32_t kBad = 0x80000000u;
+    const uint64_t per_wave = 64ull * K;
+
+    for (uint64_t base = static_cast<uint64_t>(wave) * per_wave; base < a.n; base += nwaves * per_wave) {
+        uint32_t lo_all = 0xFFFFFFFFu, hi_all = 0u;
+        for (uint32_t q = 0; q < K; ++q) {
+            const uint64_t p = base + q * 64 + lane;
+            const bool live = p < a.n;
+            uint32_t f0 = live ? a.first[p] : 0u, f1 = live ? a.first[p + 1] : 0u;
+            const bool ok = f0 <= f1 && f1 <= a.n_frags;
+            if (!ok)
+                f0 = f1 = 0;
+            const uint32_t acc = (a.seed && live) ? a.seed[p] : 0u;  // util.rs:113 (sum = initial_sum)
+            lo_all = f0 < f1 ? min(lo_all, f0) : lo_all;
+            hi_all = f0 < f1 ? max(hi_all, f1) : hi_all;
+            pk[0][q * 64 + lane] = f0;
+            pk[1][q * 64 + lane] = f1;
+            pk[2][q * 64 + lane] = acc | (ok ? 0u : kBad);
         }
-        while (acc > 0xffff)
-            acc = (acc & 0xffff) + (acc >> 16);
-        if (flags & RNS_FLAG_COMPLEMENT)
-            acc ^= 0xffff;
-        if (!ok) {
-            acc = 0;
-            if (bad)
-                atomicAdd(bad, 1u);
+        // the wave's fragments: the union of its packets' ranges (contiguous for a CSR list)
+        const uint32_t F0 = wave_min_u32(lo_all), F1 = wave_max_u32(hi_all);
+        for (uint64_t fb = F0; fb < F1; fb += 64) {
+            const uint64_t f = fb + lane;
+            uint64_t d_start = 0;
+            uint32_t d_len = 0;
+            if (f < F1) {
+                d_start = a.off[f];
+                d_len = a.len[f];
+            }
+            d_start += a.base_adjust;
+            const bool d_ok = d_start <= a.arena_bytes && d_len <= a.arena_bytes - d_start;
+            if (!d_ok || d_len == 0) {  // an empty fragment adds nothing (the reference panics on it)
+                d_len = 0;
+                d_start = 0;
+            }
+            const bool big = d_len > kNoWrapBytes, odd = d_start & 1;
+            uint32_t pos;
+            const uint32_t w = wave_class_pass<NT, BUF, kStashNone>(a, rsrc, d_start, d_len, 0u, lane, nullptr, pos);
+            uint32_t g = w;  // big: BE sum mod 2^32; else the folded BE sum (RFC 1071 §2(B), as finalize_bits)
+            if (!big) {
+                const uint32_t x = fold16(w);
+                g = odd ? x : (((x & 0xff) << 8) | (x >> 8));
+            }
+            const uint32_t gflag = (big ? 1u : 0u) | (d_ok ? 0u : 2u);
+            wave_lds_fence();
+            // owner lanes: each packet's fragments inside [fb, fb + 64), in order
+            for (uint32_t q = 0; q < K; ++q) {
+                const uint32_t i = q * 64 + lane;
+                uint64_t t = max(static_cast<uint64_t>(pk[0][i]), fb);
+                const uint64_t hi = min(static_cast<uint64_t>(pk[1][i]), fb + 64);
+                if (!__ballot(t < hi))
+                    continue;
+                uint32_t acc = pk[2][i];
+                do {
+                    const bool act = t < hi;
+                    const int src = act ? static_cast<int>(t - fb) : 0;
+                    const uint32_t gv = static_cast<uint32_t>(__shfl(static_cast<int>(g), src, 64));
+                    const uint32_t fv = static_cast<uint32_t>(__shfl(static_cast<int>(gflag), src, 64));
+                    if (act) {
+                        const uint32_t bad = (acc & kBad) | ((fv & 2u) ? kBad : 0u);
+                        uint32_t s = (acc & 0xffffu) + gv;  // big: util.rs:89-99 mod 2^32; else <= 0x1fffe
+                        if (fv & 1u) {
+                            while (s > 0xffff)  // util.rs:101-103
+                                s = (s & 0xffff) + (s >> 16);
+                        } else {
+                            s = (s & 0xffff) + (s >> 16);  // one end-around step folds it
+                        }
+                        acc = s | bad;
+                        ++t;
+                    }
+                } while (__ballot(t < hi));
+                pk[2][i] = acc;
+            }
         }
-        out[i] = static_cast<uint16_t>(acc);
+        wave_lds_fence();
+        for (uint32_t q = 0; q < K; ++q) {
+            const uint64_t p = base + q * 64 + lane;
+            const uint32_t acc = pk[2][q * 64 + lane];
+            uint32_t r = acc & 0xffffu;
+            if (a.flags & RNS_FLAG_COMPLEMENT)
+                r ^= 0xffff;
+            const bool ok = !(acc & kBad);
+            if (p < a.n)
+                a.out[p] = static_cast<uint16_t>(ok ? r : 0u);  // 64 consecutive u16: one 128-byte store
+            if (a.bad) {
+                const uint64_t rejected = __ballot(p < a.n && !ok);
+                if (rejected && lane == 0)
+                    atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
+            }
+        }
+        wave_lds_fence();  // the next batch rewrites pk
     }
 }
 
@@ -1325,7 +1535,8 @@ __global__ __launch_bounds__(kBlock) void splitmix64_fill_kernel(uint8_t *buf, u
 inline int hip_status(hipError_t e) { return e == hipSuccess ? RNS_OK : RNS_E_HIP_BASE - static_cast<int>(e); }
 
 // Kernel variants: bit 0 = rounds kernel (1) / group kernel (0); bit 1 = nontemporal loads;
-// bit 2 = mixed kernel; bit 3 = rounds kernel with every round in flight.
+// bit 2 = mixed kernel; bit 3 = rounds kernel with every round in flight; bit 4 = rounds
+// kernel with the next batch's descriptors prefetched.
 template <int G, int U, bool S>
 int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipStream_t st)
 {
@@ -1380,6 +1591,20 @@ int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipSt
         } else {
             return RNS_E_INVALID;
         }
+    } else if (variant & 16) {  // rounds kernel, next batch's descriptors prefetched (tiny packets)
+        if constexpr (G <= 8 && U <= 2) {
+            if (nt && buf)
+                hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, true, 1, false, true>), grid, block, lds, st, a);
+            else if (nt)
+                hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, false, 1, false, true>), grid, block, lds, st, a);
+            else if (buf)
+                hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, false, true, 1, false, true>), grid, block, lds, st, a);
+            else
+                hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, false, false, 1, false, true>), grid, block, lds, st,
+                                   a);
+        } else {
+            return RNS_E_INVALID;
+        }
     } else {
         if (nt && buf)
             hipLaunchKernelGGL((csum_rounds_kernel<G, U, S, true, true>), grid, block, lds, st, a);
@@ -1397,7 +1622,8 @@ template <bool S>
 int dispatch(const CsumArgs &a, uint32_t variant, uint32_t G, uint32_t U, uint32_t max_blocks, hipStream_t st)
 {
     const uint32_t v = variant & 0xffu;  // bits 8-11: occupancy cap (launch_shape)
-    if (v > 15 || (variant >> 12) || ((v & 8) && (v & 5) != 1))  // bit 3 (deep prefetch): rounds kernel only
+    // bit 3 (deep prefetch) and bit 4 (descriptor prefetch): rounds kernel only, not both
+    if (v > 31 || (variant >> 12) || ((v & 24) && (v & 5) != 1) || (v & 24) == 24)
         return RNS_E_INVALID;
     if (variant & 4)  // the mixed kernel picks its own per-class shapes
         return launch_shape<64, 4, S>(a, variant, max_blocks, st);
@@ -1415,9 +1641,13 @@ int dispatch(const CsumArgs &a, uint32_t variant, uint32_t G, uint32_t U, uint32
     return RNS_E_INVALID;
 }
 
+struct Shape;
+int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st);
+
 // Kernel shape for a typical (mean) packet length, in 16-byte chunks, from the
 // interleaved shape sweeps on MI355X (tools/sweep_shapes.py, profiles/r01_sweep*.json):
-//   <= 8 chunks   (64 B)        rounds, nontemporal, G=4, U=1, grid 2048      (c2)
+//   <= 8 chunks   (64 B)        rounds, nontemporal, G=4, U=1, grid 2048,     (c2)
+//                               next batch's descriptors prefetched
 //   <= 48 chunks  (IMIX mean)   mixed (per-wave size-class sort)              (c5)
 //   <= 160 chunks (1500 B)      mixed, nontemporal (= rounds G=32,U=4 here)   (c3, headline)
 //   longer        (9000 B)      group, nontemporal, G=64, U=4                 (c4)
@@ -1430,13 +1660,50 @@ struct Shape {
 Shape pick_shape(uint32_t len_hint)
 {
     const uint32_t chunks = len_hint ? (len_hint + 15) / 16 + 1 : 96;
-    if (chunks <= 8)
-        return Shape{3u, 4u, 1u, 2048u};
+    if (chunks <= 8)  // rounds, nontemporal, next batch's descriptors prefetched (c2: 15.1 -> 14.4 us)
+        return Shape{19u, 4u, 1u, 2048u};
     if (chunks <= 48)
         return Shape{4u, 0u, 0u, 0u};
     if (chunks <= 160)
         return Shape{6u, 0u, 0u, 0u};
     return Shape{2u, 64u, 4u, 0u};
+}
+
+// The packed form's kernels (separate instantiations, so the explicit-descriptor
+// kernels carry no packed-form code): the mixed kernel, or for tiny packets the
+// rounds kernel with pick_shape's G=4, U=1 shape.
+int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
+{
+    const bool nt = (sh.variant & 2u) != 0, buf = buf_records(a) < kOobOffset;
+    const uint64_t batches = (static_cast<uint64_t>(a.n) + 63) / 64;  // one wave per 64 packets
+    uint64_t blocks = (batches + kBlock / 64 - 1) / (kBlock / 64);
+    if (sh.max_blocks != 0 && blocks > sh.max_blocks)
+        blocks = sh.max_blocks;
+    const dim3 grid(static_cast<uint32_t>(blocks)), block(kBlock);
+    if (sh.variant & 4u) {
+        if (nt && buf)
+            hipLaunchKernelGGL((csum_mixed_kernel<false, true, true, false, false, false, true>), grid, block, 0, st, a);
+        else if (nt)
+            hipLaunchKernelGGL((csum_mixed_kernel<false, true, false, false, false, false, true>), grid, block, 0, st, a);
+        else if (buf)
+            hipLaunchKernelGGL((csum_mixed_kernel<false, false, true, false, false, false, true>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_mixed_kernel<false, false, false, false, false, false, true>), grid, block, 0, st,
+                               a);
+    } else if ((sh.variant & ~16u) == 3u && sh.G == 4u && sh.U == 1u) {  // c2: 13.46 -> 13.36 us with prefetch
+        const bool pf = (sh.variant & 16u) != 0;
+        if (buf && pf)
+            hipLaunchKernelGGL((csum_rounds_kernel<4, 1, false, true, true, 1, true, true>), grid, block, 0, st, a);
+        else if (buf)
+            hipLaunchKernelGGL((csum_rounds_kernel<4, 1, false, true, true, 1, true>), grid, block, 0, st, a);
+        else if (pf)
+            hipLaunchKernelGGL((csum_rounds_kernel<4, 1, false, true, false, 1, true, true>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_rounds_kernel<4, 1, false, true, false, 1, true>), grid, block, 0, st, a);
+    } else {
+        return RNS_E_INVALID;
+    }
+    return hip_status(hipGetLastError());
 }
 
 int check_device()
@@ -1575,6 +1842,33 @@ int rns_csum_batch_dev_off32(const uint8_t *d_arena, uint64_t arena_bytes, const
     return dispatch<false>(a, sh.variant, sh.G, sh.U, sh.max_blocks, static_cast<hipStream_t>(stream));
 }
 
+int rns_csum_batch_packed_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_blk_off,
+                              const uint16_t *d_len16, uint32_t align_log2, const uint16_t *d_seed, uint16_t *d_out,
+                              uint32_t n, uint32_t flags, uint32_t len_hint, uint32_t *d_bad, void *stream)
+{
+    if (n == 0)
+        return RNS_OK;
+    if (!d_arena || !d_blk_off || !d_len16 || !d_out || align_log2 > 12)
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    Shape sh = pick_shape(len_hint);
+    if ((sh.variant & 5u) == 0)  // the group kernel has no 64-packet wave batches: mixed kernel, nontemporal
+        sh = Shape{6u, 0u, 0u, 0u};
+
+    CsumArgs a{};
+    set_arena(a, d_arena, arena_bytes);
+    a.len16 = d_len16;
+    a.blk_off = d_blk_off;
+    a.align_mask = (1u << align_log2) - 1u;
+    a.seed = d_seed;
+    a.out = d_out;
+    a.bad = d_bad;
+    a.n = n;
+    a.flags = flags;
+    return dispatch_packed(a, sh, static_cast<hipStream_t>(stream));
+}
+
 int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uint64_t first_off,
                                uint64_t stride, uint32_t len, const uint16_t *d_seed, uint16_t *d_out,
                                uint32_t n, uint32_t flags, uint32_t *d_bad, void *stream)
@@ -1604,32 +1898,59 @@ int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
                        const uint16_t *d_seed, uint16_t *d_out, uint32_t n_pkts, uint32_t flags,
                        uint32_t frag_len_hint, uint16_t *d_frag_sums, uint32_t *d_bad, void *stream)
 {
+    (void)d_frag_sums;  // scratch of the two-pass form (round 1); the one-pass kernel needs none
     if (n_pkts == 0)
         return RNS_OK;
-    if (!d_arena || !d_first || !d_out || (n_frags && (!d_frag_off || !d_frag_len || !d_frag_sums)))
+    if (!d_arena || !d_first || !d_out || (n_frags && (!d_frag_off || !d_frag_len)))
         return RNS_E_INVALID;
     if (int st = check_device())
         return st;
-    // pass 1: every fragment as its own packet, seed 0, not complemented, no bad counting here
-    if (n_frags) {
-        const Shape sh = pick_shape(frag_len_hint ? frag_len_hint : 512u);
-        CsumArgs a{};
-        set_arena(a, d_arena, arena_bytes);
-        a.off = d_frag_off;
-        a.len = d_frag_len;
-        a.seed = nullptr;
-        a.out = d_frag_sums;
-        a.bad = nullptr;
-        a.n = n_frags;
-        a.flags = 0;
-        if (int st = dispatch<false>(a, sh.variant, sh.G, sh.U, sh.max_blocks, static_cast<hipStream_t>(stream)))
-            return st;
+    CsumArgs a{};
+    set_arena(a, d_arena, arena_bytes);
+    a.off = d_frag_off;
+    a.len = d_frag_len;
+    a.seed = d_seed;
+    a.out = d_out;
+    a.bad = d_bad;
+    a.n = n_pkts;
+    a.flags = flags;
+    a.first = d_first;
+    a.n_frags = n_frags;
+    // Packets per lane K: the wave's K*64 packets should bring whole 64-fragment
+    // batches (a partial batch runs the class rounds for few bytes), so pick the K
+    // in 1..8 whose expected fragment count K*mean fills its batches best.
+    const double mean = static_cast<double>(n_frags) / static_cast<double>(n_pkts);
+    uint32_t K = 1;
+    double best = -1.0;
+    for (uint32_t k = 1; k <= kChainMaxK; ++k) {
+        const double fr = k * mean, fill = fr > 0 ? fr / std::ceil(fr) : 1.0;
+        if (fill > best + 0.02) {
+            best = fill;
+            K = k;
+        }
     }
-    // pass 2: chain per packet
-    const uint32_t blocks = static_cast<uint32_t>(std::min<uint64_t>((n_pkts + kBlock - 1) / kBlock, 4096));
-    hipLaunchKernelGGL(chain_combine_kernel, dim3(blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
-                       d_frag_off, d_frag_len, d_frag_sums, n_frags, d_first, d_seed, d_out, n_pkts, arena_bytes,
-                       flags, d_bad);
+    a.chain_k = K;
+    const uint64_t waves = (static_cast<uint64_t>(n_pkts) + 64 * K - 1) / (64 * K);
+    const dim3 grid(static_cast<uint32_t>((waves + kBlock / 64 - 1) / (kBlock / 64))), block(kBlock);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    // nontemporal loads for long fragments, as pick_shape chooses for packets
+    const bool nt = pick_shape(frag_len_hint ? frag_len_hint : 512u).variant & 2u;
+    const bool buf = buf_records(a) < kOobOffset;
+#define RNS_CHAIN_LAUNCH(KM)                                                                      \
+    if (nt && buf)                                                                                \
+        hipLaunchKernelGGL((csum_chain_kernel<true, true, KM>), grid, block, 0, st, a);           \
+    else if (nt)                                                                                  \
+        hipLaunchKernelGGL((csum_chain_kernel<true, false, KM>), grid, block, 0, st, a);          \
+    else if (buf)                                                                                 \
+        hipLaunchKernelGGL((csum_chain_kernel<false, true, KM>), grid, block, 0, st, a);          \
+    else                                                                                          \
+        hipLaunchKernelGGL((csum_chain_kernel<false, false, KM>), grid, block, 0, st, a);
+    if (K == 1) {
+        RNS_CHAIN_LAUNCH(1)
+    } else {
+        RNS_CHAIN_LAUNCH(kChainMaxK)
+    }
+#undef RNS_CHAIN_LAUNCH
     return hip_status(hipGetLastError());
 }
 
@@ -2042,7 +2363,8 @@ const char *rns_csum_shape_name(uint32_t len_hint)
         std::snprintf(buf, sizeof(buf), "%s (size classes G/U 4/1, 4/4, 16/4, 32/4, 64/4)", names[sh.variant & 7]);
     else
         std::snprintf(buf, sizeof(buf), "%s<G=%u,U=%u>%s%s", names[sh.variant & 7], sh.G, sh.U,
-                      (sh.variant & 8) ? " all rounds in flight" : "", sh.max_blocks ? " grid-capped" : "");
+                      (sh.variant & 8) ? " all rounds in flight" : (sh.variant & 16) ? " descriptors prefetched" : "",
+                      sh.max_blocks ? " grid-capped" : "");
     return buf;
 }
 
@@ -2050,7 +2372,8 @@ const char *rns_build_info(void)
 {
     return "rns_checksum abi=1 offload-arch=gfx950 kernels=csum_mixed_kernel (per-wave size-class sort; "
            "verify / fill / transmit-finalize stash modes), csum_rounds_kernel, csum_batch_kernel, "
-           "chain_combine_kernel (v_sad_u16 LE sums, v_dot4 BE sums past 128 KiB, wave64, DPP reductions)";
+           "csum_chain_kernel (one pass, per-fragment fold) (v_sad_u16 LE sums, v_dot4 BE sums past 128 KiB, wave64, "
+           "DPP reductions)";
 }
 
 int rns_device_count(void)

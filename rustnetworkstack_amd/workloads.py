@@ -130,14 +130,29 @@ class DeviceBatch:
         self.out = torch.empty(layout.n, dtype=torch.uint16, device=self.device)
         self._prepared = {}
 
-    def launcher(self, complement: bool = False, shape=None, compact: bool = False):
+    def launcher(self, complement: bool = False, shape=None, compact: bool = False, packed: bool = False):
         """Pre-bound launch (one ctypes call per launch) on the current stream.
-        ``compact`` binds 32-bit offsets (rns_csum_batch_dev_off32; arenas < 4 GiB)."""
+        ``compact`` binds 32-bit offsets (rns_csum_batch_dev_off32; arenas < 4 GiB);
+        ``packed`` binds the packed form (rns_csum_batch_packed_dev: u16 lengths + one
+        offset per 64 packets; the synthetic layouts ARE packed at 16-byte alignment)."""
         import torch
 
-        from .batch import PreparedBatch
-        key = (complement, shape, compact)
+        from .batch import PackedBatch, PreparedBatch, packed_layout
+        key = (complement, shape, compact, packed)
         if key not in self._prepared:
+            if packed:
+                if shape is not None or compact:
+                    raise ValueError("the packed form takes no shape override and no compact offsets")
+                blk, off, _ = packed_layout(self.layout.length, align_log2=ALIGN.bit_length() - 1,
+                                            first_off=int(self.layout.off[0]) if self.layout.n else 0)
+                if not np.array_equal(off, self.layout.off):
+                    raise ValueError("layout is not packed at the default alignment")
+                self.blk_off = torch.from_numpy(blk.view(np.int64)).to(self.device)
+                self.len16 = torch.from_numpy(self.layout.length.astype(np.uint16).view(np.int16)).to(self.device)
+                self._prepared[key] = PackedBatch(self.arena, self.blk_off, self.len16, self.seed,
+                                                  align_log2=ALIGN.bit_length() - 1, complement=complement,
+                                                  out=self.out, len_hint=int(round(self.layout.mean_len)))
+                return self._prepared[key]
             off = self.off
             if compact:
                 if self.layout.arena_bytes + 16 >= 2 ** 32:

@@ -44,6 +44,7 @@ class CpuEngine(bench.GpuEngine):
         self.batches = [_Batch(self.layout)]
         self.last = self.batches[0]
         self.compact, self.shape, self.k, self.timed = True, None, 0, 0
+        self.packed, self.form = False, "32"
         self.gatherer = None
         self.orc = get_oracle()
         ENGINES.append(self)

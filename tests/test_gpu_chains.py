@@ -103,3 +103,90 @@ def test_bad_fragment_rejects_packet():
     bad = torch.zeros(1, dtype=torch.int32, device=DEV)
     got = run_chain(a, [0, 4000, 10], [16, 200, 4], [0, 2, 3], [5, 6], bad=bad)
     assert got[0] == 0 and got[1] == 6 and int(bad.item()) == 1
+
+
+def test_many_fragments_no_overflow(oracle):
+    """70 000 one-byte 0xff fragments in one packet (each adds the word 0xff00): the
+    reference folds after every fragment (util.rs:113-118), so its running sum never
+    overflows; a one-fold-at-the-end combine would wrap past 65 537 fragments."""
+    arena_np = np.full(70_000 + 64, 0xff, dtype=np.uint8)
+    nfr = 70_000
+    offs = np.arange(nfr, dtype=np.uint64)
+    lens = np.ones(nfr, dtype=np.uint32)
+    # packet 0: the 70 000 fragments; packets 1-3: short chains after it (same wave)
+    offs = np.concatenate([offs, np.array([70_000, 70_001, 70_010, 70_020], dtype=np.uint64)])
+    lens = np.concatenate([lens, np.array([1, 9, 10, 33], dtype=np.uint32)])
+    first = np.array([0, nfr, nfr + 2, nfr + 3, nfr + 4], dtype=np.uint32)
+    seeds = np.array([0xfffe, 1, 0, 0xffff], dtype=np.uint16)
+    for complement in (False, True):
+        expect = oracle.chain_batch(arena_np, offs, lens, first, seeds, complement=complement)
+        got = run_chain(torch.from_numpy(arena_np).to(DEV), offs, lens, first, seeds, complement=complement)
+        assert np.array_equal(got, expect)
+
+
+@pytest.mark.parametrize("fill", [0xff, None])
+def test_big_fragment_after_nonzero_running_sum(oracle, fill):
+    """A fragment longer than 128 KiB after a fragment that leaves a nonzero running
+    sum: the reference's u32 accumulator starts from that sum and wraps (release
+    build), which a per-fragment sum from seed 0 cannot reproduce."""
+    big = 200_001
+    if fill is None:
+        arena_np = O.splitmix64_bytes(0xB16, big + 4096)
+    else:
+        arena_np = np.full(big + 4096, fill, dtype=np.uint8)
+    offs = np.array([0, 7, 7 + 1000, 3, 4000, 11, 1], dtype=np.uint64)
+    lens = np.array([7, 1000, big, 1, big - 900, 3, big + 11], dtype=np.uint32)
+    first = np.array([0, 3, 5, 7], dtype=np.uint32)   # [7 B, 1000 B, big], [1 B, big-900], [3 B, big+11]
+    for seeds in (np.array([0xffff, 0x1234, 0], dtype=np.uint16), None):
+        expect = oracle.chain_batch(arena_np, offs, lens, first, seeds, complement=True)
+        got = run_chain(torch.from_numpy(arena_np).to(DEV), offs, lens, first, seeds, complement=True)
+        assert np.array_equal(got, expect)
+
+
+def test_random_chains_mixed_sizes_and_malformed(oracle):
+    """30K chains: 0-12 fragments of 0..3000 B with an occasional jumbo fragment
+    (past 128 KiB), empty fragments, and a few malformed CSR ranges (end < start,
+    end past n_frags), whose packets must come back 0 and be counted in *bad."""
+    n = 30_000
+    size = 8 << 20
+    arena_np = O.splitmix64_bytes(0xC5A1, size)
+    w = O.splitmix64_words(0xC5A2, n)
+    nfr = (w % np.uint64(13)).astype(np.int64)
+    first = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(nfr, out=first[1:])
+    nf = int(first[-1])
+    fw = O.splitmix64_words(0xC5A3, nf)
+    lens = (fw % np.uint64(3001)).astype(np.uint32)
+    jumbo = (fw >> np.uint64(50)) % np.uint64(97) == 0
+    lens[jumbo] = (140_000 + (fw[jumbo] >> np.uint64(8)) % np.uint64(300_000)).astype(np.uint32)
+    offs = ((fw >> np.uint64(20)) % np.uint64(size - 450_000)).astype(np.uint64)
+    seeds = (w >> np.uint64(40) & np.uint64(0xFFFF)).astype(np.uint16)
+    first = first.astype(np.uint32)
+    first[18] = first[17] + 20 if first[17] + 20 <= nf else nf   # packet 18 starts past where it ends
+    first[19] = first[18] - 3                                     # (packet 18: end < start)
+    first[4001] = nf + 5                                          # packets 4000/4001: end past n_frags / < start
+    first[n] = nf + 1                                             # the last packet: end past n_frags
+    lo, hi = first[:-1].astype(np.int64), first[1:].astype(np.int64)
+    valid = (lo <= hi) & (hi <= nf)
+    # expected: the oracle over each valid packet's own fragment range
+    idx = [np.arange(a, b) for a, b in zip(lo[valid], hi[valid])]
+    sub_first = np.zeros(int(valid.sum()) + 1, dtype=np.uint32)
+    np.cumsum([len(i) for i in idx], out=sub_first[1:])
+    cat = np.concatenate(idx) if idx else np.zeros(0, dtype=np.int64)
+    expect = oracle.chain_batch(arena_np, offs[cat], lens[cat], sub_first, seeds[valid], complement=True)
+    bad = torch.zeros(1, dtype=torch.int32, device=DEV)
+    got = run_chain(torch.from_numpy(arena_np).to(DEV), offs, lens, first, seeds, complement=True, bad=bad)
+    assert (~valid).sum() >= 4
+    assert np.array_equal(got[valid], expect)
+    assert (got[~valid] == 0).all()
+    assert int(bad.item()) == int((~valid).sum())
+
+
+def test_packets_without_fragments():
+    """Packets with no fragments return their seed (complemented on request); a batch
+    with no fragments at all never reads the fragment arrays."""
+    a = torch.zeros(64, dtype=torch.uint8, device=DEV)
+    got = run_chain(a, [], [], [0] * 101, list(range(100)))
+    assert np.array_equal(got, np.arange(100, dtype=np.uint16))
+    got = run_chain(a, [], [], [0] * 101, list(range(100)), complement=True)
+    assert np.array_equal(got, (0xffff ^ np.arange(100)).astype(np.uint16))

@@ -1,0 +1,126 @@
+"""Packed descriptors (rns_csum_batch_packed_dev: u16 lengths, offsets implied by
+the lengths and the alignment, one base offset per 64 packets) against the oracle
+and against the 64-bit descriptor path, through the C ABI.
+
+Per packet the arithmetic is util.rs:88-110 exactly as for rns_csum_batch_dev; only
+how a packet's offset is found differs (a wave-wide scan of padded lengths), so
+every case here must be bit-exact with the golden fixtures / the C oracle.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import sweep_arena
+from oracle import oracle as O
+from rustnetworkstack_amd import _lib
+from rustnetworkstack_amd.batch import csum_batch, csum_batch_packed, packed_layout
+from rustnetworkstack_amd.workloads import DeviceBatch, make_layout
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def host_u16(t: torch.Tensor) -> np.ndarray:
+    torch.cuda.synchronize()
+    return t.view(torch.int16).cpu().numpy().view(np.uint16)
+
+
+def dev(a: np.ndarray, view) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a).view(view)).to(DEV)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu_present():
+    if not torch.cuda.is_available() or _lib.load().rns_device_count() == 0:
+        pytest.fail("gpu tests need a GPU (the HIP path has no CPU fallback)")
+
+
+def pack(src: np.ndarray, off: np.ndarray, length: np.ndarray, align_log2: int, first_off: int = 0,
+         filler: int = 0xA5):
+    """Copy packets (src[off:off+len]) into a packed arena; padding bytes get `filler`
+    (never zero: the kernels must not count them)."""
+    blk, poff, end = packed_layout(length, align_log2, first_off)
+    arena = np.full(end + 16, filler, dtype=np.uint8)
+    for o, po, n in zip(off.tolist(), poff.tolist(), length.tolist()):
+        arena[po:po + n] = src[o:o + n]
+    return arena, blk, poff
+
+
+def run_packed(arena_np, blk, length, seed, align_log2, complement=False, len_hint=0, bad=None, arena_bytes=None):
+    arena = torch.from_numpy(arena_np).to(DEV)
+    if arena_bytes is not None:
+        arena = arena[:arena_bytes]
+    return host_u16(csum_batch_packed(arena, dev(blk.astype(np.uint64), np.int64),
+                                      dev(np.asarray(length).astype(np.uint16), np.int16),
+                                      None if seed is None else dev(np.asarray(seed).astype(np.uint16), np.int16),
+                                      align_log2=align_log2, complement=complement, len_hint=len_hint, bad=bad))
+
+
+@pytest.mark.parametrize("align_log2", [0, 1, 2, 4, 6, 12])
+def test_golden_sweep_packed(sweep, align_log2):
+    """The golden sweep's packets (lengths 1..2048, 9000, edge patterns) repacked at
+    every alignment, including byte-packed (odd starts) and page-aligned."""
+    src = sweep_arena(sweep)
+    off = np.array(sweep["offset"], dtype=np.uint64)
+    ln = np.array(sweep["length"], dtype=np.uint32)
+    keep = ln <= 0xFFFF
+    off, ln = off[keep], ln[keep]
+    sd = np.array(sweep["pkt_seed"], dtype=np.uint16)[keep]
+    expect = np.array(sweep["expect"], dtype=np.uint16)[keep]
+    arena, blk, _ = pack(src, off, ln, align_log2, first_off=7 if align_log2 == 0 else 0)
+    for hint in (0, 40, 64, 576, 1500, 9000):
+        assert np.array_equal(run_packed(arena, blk, ln, sd, align_log2, len_hint=hint), expect), hint
+        assert np.array_equal(run_packed(arena, blk, ln, sd, align_log2, complement=True, len_hint=hint),
+                              expect ^ 0xFFFF), hint
+
+
+def test_random_lengths_any_alignment(oracle):
+    """Lengths 0..65535 (mostly short), several alignments, n not a multiple of 64,
+    a nonzero first offset; every packet against the C oracle."""
+    rng = np.random.default_rng(0x9AC)
+    n = 20_011
+    ln = np.where(rng.random(n) < 0.9, rng.integers(0, 1600, n), rng.integers(0, 65536, n)).astype(np.uint32)
+    sd = rng.integers(0, 1 << 16, n).astype(np.uint16)
+    for align_log2, first in ((0, 3), (3, 8), (4, 48), (7, 128)):
+        blk, poff, end = packed_layout(ln, align_log2, first)
+        arena = O.splitmix64_bytes(0x9AC0 + align_log2, end + 16)
+        expect = oracle.batch(arena, poff, ln, sd, complement=True)
+        for hint in (0, 64, 340, 1500, 9000):
+            got = run_packed(arena, blk, ln, sd, align_log2, complement=True, len_hint=hint)
+            assert np.array_equal(got, expect), (align_log2, hint)
+
+
+def test_packets_past_the_arena_are_rejected():
+    """A packed arena cut short: the packets that end past it get 0 and are counted."""
+    rng = np.random.default_rng(7)
+    n = 300
+    ln = rng.integers(1, 1500, n).astype(np.uint32)
+    blk, poff, end = packed_layout(ln, 4)
+    arena = O.splitmix64_bytes(77, end + 16)
+    cut = int(poff[200]) + 5  # packet 200 and everything after it no longer fit
+    bad = torch.zeros(1, dtype=torch.int32, device=DEV)
+    got = run_packed(arena, blk, ln, None, 4, len_hint=600, bad=bad, arena_bytes=cut)
+    expect = O.get_oracle().batch(arena[:cut], poff[:200], ln[:200], None)
+    assert np.array_equal(got[:200], expect)
+    assert (got[200:] == 0).all()
+    assert int(bad.item()) == n - 200
+
+
+def test_packed_layout_rejects_long_lengths():
+    with pytest.raises(ValueError):
+        packed_layout(np.array([70000]), 4)
+
+
+@pytest.mark.parametrize("name", ["c2_64B", "c3_1500B", "c4_9000B", "c5_imix"])
+def test_full_size_packed_equals_64bit(name):
+    """Every packet of each BASELINE.json config (the synthetic layouts are packed at
+    16 bytes): packed == 64-bit descriptors, which test_gpu_parity checks packet by
+    packet against the oracle."""
+    lay = make_layout(name)
+    b = DeviceBatch(lay, DEV)
+    ref = csum_batch(b.arena, b.off, b.length, b.seed, complement=True, len_hint=int(lay.mean_len))
+    got = b.launcher(complement=True, packed=True)()
+    assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+    del b
+    torch.cuda.empty_cache()

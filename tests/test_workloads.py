@@ -42,3 +42,25 @@ def test_sharding_covers_every_packet_once():
         assert sum(p.n for p in parts) == full.n
         assert np.array_equal(np.concatenate([p.length for p in parts]), full.length)
         assert np.array_equal(np.concatenate([p.seed for p in parts]), full.seed)
+
+
+def test_packed_layout_matches_synthetic_offsets():
+    """rns_packed_layout (host C ABI) reproduces every synthetic config's offsets at
+    16-byte alignment, and implements align_up(previous end) at any alignment."""
+    import numpy as np
+
+    from rustnetworkstack_amd.batch import packed_layout
+    from rustnetworkstack_amd.workloads import make_layout
+    for name, n in (("c2_64B", 1000), ("c3_1500B", 1000), ("c5_imix", 4099)):
+        lay = make_layout(name, n=n)
+        blk, off, end = packed_layout(lay.length, 4)
+        assert np.array_equal(off, lay.off) and end == lay.arena_bytes
+        assert np.array_equal(blk, lay.off[::64])
+    rng = np.random.default_rng(3)
+    ln = rng.integers(0, 65536, 777)
+    for a in (0, 1, 5, 12):
+        blk, off, end = packed_layout(ln, a, first_off=9)
+        m = (1 << a) - 1
+        expect = 9 + np.concatenate([[0], np.cumsum((ln + m) & ~m)])
+        assert np.array_equal(off, expect[:-1]) and end == int(expect[-1])
+        assert np.array_equal(blk, off[::64])

@@ -79,6 +79,9 @@ def main():
     ap.add_argument("--configs", default="c3_1500B,c5_imix")
     ap.add_argument("--ops", default="csum,chain,fill,verify,tx")
     ap.add_argument("--out", default="")
+    ap.add_argument("--chain-layouts", default="packed,netbuf",
+                    help="packed: [492, 512, rest] fragments back to back inside each packet; netbuf: every "
+                         "fragment in its own 512-byte buffer (NetBuffer, buf.rs:50), ceil(L/512) per packet")
     args = ap.parse_args()
     ops = set(args.ops.split(","))
     dev = torch.device("cuda:0")
@@ -94,7 +97,9 @@ def main():
             ms = timed(pb, args.steps, args.rounds)
             r["csum"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1)}
         if "chain" in ops:
-            r["chain"] = bench_chain(b, lay, dev, args)
+            for cl in args.chain_layouts.split(","):
+                key = "chain" if cl == "packed" else f"chain_{cl}"
+                r[key] = bench_chain(b, lay, dev, args) if cl == "packed" else bench_chain_netbuf(lay, dev, args)
         if "fill" in ops:
             ms = timed(lambda: csum_fill(b.arena, b.off, b.length, b.seed, field_off=16), args.steps, args.rounds)
             r["fill"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1)}
@@ -156,6 +161,37 @@ def bench_chain(b, lay, dev, args):
                                   frag_sums=sums, frag_len_hint=int(round(pay / nf))),
                args.steps, args.rounds)
     return {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1), "fragments": nf}
+
+
+def bench_chain_netbuf(lay, dev, args):
+    """Fragments as NetBuffer holds them: packet i of L bytes is ceil(L/512) fragments,
+    each in its own 512-byte buffer (buf.rs:50; the fragment arena is those buffers
+    back to back, filled with splitmix64 bytes)."""
+    from rustnetworkstack_amd.batch import fill_splitmix64
+    n, pay = lay.n, lay.payload_bytes
+    L = lay.length.astype(np.int64)
+    nfr = (L + 511) // 512
+    first = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(nfr, out=first[1:])
+    nf = int(first[-1])
+    pkt = np.repeat(np.arange(n), nfr)
+    k = np.arange(nf) - first[:-1][pkt]
+    frag_off = (np.arange(nf, dtype=np.uint64) * np.uint64(512))
+    frag_len = np.minimum(L[pkt] - 512 * k, 512).astype(np.uint32)
+    arena = torch.empty(nf * 512 + 16, dtype=torch.uint8, device=dev)
+    fill_splitmix64(arena, 0xF4A6)
+    d_fo = torch.from_numpy(frag_off.view(np.int64)).to(dev)
+    d_fl = torch.from_numpy(frag_len.view(np.int32)).to(dev)
+    d_first = torch.from_numpy(first.astype(np.uint32).view(np.int32)).to(dev)
+    seed = torch.from_numpy(lay.seed.view(np.int16)).to(dev)
+    out = torch.empty(n, dtype=torch.uint16, device=dev)
+    ms = timed(lambda: csum_chain(arena, d_fo, d_fl, d_first, seed, complement=True, out=out,
+                                  frag_len_hint=int(round(pay / nf))),
+               args.steps, args.rounds)
+    del arena
+    torch.cuda.empty_cache()
+    return {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1), "fragments": nf,
+            "layout": "netbuf: 512-byte fragment buffers"}
 
 
 if __name__ == "__main__":
