@@ -18,6 +18,11 @@ separately: `value_gather` = the same steps with one RCCL all-gather of every
 rank's u16 results (as uint8, 2 B per packet) per step, and `gather_ms` = the
 all-gather alone.  Rank 0 prints one JSON line.
 
+Descriptors (--desc auto): the packed form (rns_csum_batch_packed_dev: u16 length and
+u16 seed per packet, one u64 offset per 64 packets) — the synthetic batches are packed
+at 16-byte alignment — except for jumbo batches, whose group kernel has no 64-packet
+wave batches: they take the compact form (u32 offsets).
+
 Kernel time: one event pair around the K back-to-back timed launches gives the
 per-launch mean (`kernel_avg_us`) from which `roofline.frac` is computed.  A
 rocprofv3 --kernel-trace of the same command reproduces it (tools/profile_bench.py
@@ -62,6 +67,15 @@ def parse_args(argv=None):
     p.add_argument("--median-launches", type=int, default=0,
                    help="diagnostic: N extra launches each inside its own event pair, median reported "
                         "(pairs add ~5 us per launch; 0 = skip)")
+    p.add_argument("--ramp-s", type=float, default=0.5,
+                   help="before the W warmup steps, repeat the step (untimed) for this many seconds so the "
+                        "GPU leaves its idle clock state: a 2.9 GB IMIX launch takes 505-550 us in the first "
+                        "~0.1 s of load and 493-496 us after it (profiles/r02_clock_ramp.json); 0 = off")
+    p.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
+                   help="launch the K timed steps (and the warmup) as one HIP graph of K kernel launches "
+                        "(torch.cuda.CUDAGraph): no host launch cost between steps; auto = on for batches "
+                        "small enough to rotate (c2), whose ~13 us kernels the host cannot launch one by one "
+                        "fast enough")
     p.add_argument("--scaling", choices=("auto", "weak", "strong"), default="auto",
                    help="weak: every rank checksums a full batch of the config; strong: the config's batch is "
                         "sharded by packet index across ranks (auto: strong for c5_imix, whose BASELINE.json "
@@ -124,22 +138,47 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def timed_loop(engine, dist: Dist, steps: int, warmup: int, step=None) -> dict:
+def clock_ramp(engine, seconds: float, step=None, graph=None) -> int:
+    """Untimed load for `seconds` of wall time before the warmup steps (DVFS: the chip
+    runs its first ~0.1 s of load at lower clocks).  Returns the steps run."""
+    step = step or engine.step
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(8):
+            if graph is not None:
+                graph.replay()
+            else:
+                step()
+        engine.sync()
+        n += 8
+    return n
+
+
+def timed_loop(engine, dist: Dist, steps: int, warmup: int, step=None, graph=None) -> dict:
     """W untimed steps, then exactly K steps bracketed by sync + barrier on both
     sides; wall time is the max over ranks.  Device time per launch = one pair of
     events on the launch stream around the K back-to-back launches, / K (events
     between launches would insert ~10 µs gaps: see DESIGN.md, measurement).
-    `step` (default engine.step) is what one step runs."""
+    `step` (default engine.step) is what one step runs; `graph` (optional) = a
+    captured graph of exactly K steps, replayed once for the timed region (and
+    once untimed as warmup when W > 0)."""
     step = step or engine.step
-    for _ in range(warmup):
-        step()
+    if graph is not None:
+        if warmup:
+            graph.replay()
+    else:
+        for _ in range(warmup):
+            step()
     engine.sync()
     dist.barrier()
     engine.sync()
     t0 = time.perf_counter()
     engine.begin_timing()
-    for _ in range(steps):
-        step()
+    if graph is not None:
+        graph.replay()
+    else:
+        for _ in range(steps):
+            step()
     engine.end_timing(steps)
     engine.sync()
     dist.barrier()
@@ -263,6 +302,23 @@ class GpuEngine:
         self.k += 1
         b.launcher(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)()  # one ctypes call
         self.last = b
+
+    def capture(self, steps: int):
+        """K steps captured as one HIP graph (K kernel launches, rotating batches in
+        step order), each launcher re-bound to the capture stream."""
+        torch = self.torch
+        fns = [b.rebind(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)
+               for b in self.batches]
+        del fns  # (bound once outside the capture: descriptor uploads happen here, not inside it)
+        self.sync()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for i in range(steps):
+                b = self.batches[i % len(self.batches)]
+                b.rebind(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)()
+        self.sync()
+        self.last = self.batches[(steps - 1) % len(self.batches)]
+        return g
 
     def gather(self):
         """The all-gather of the results of the batch the last step checksummed."""
@@ -452,7 +508,10 @@ def main(argv=None):
     strong = args.scaling == "strong" or (args.scaling == "auto" and args.config == "c5_imix")
     engine = GpuEngine(args.config, dist.rank, dist.local_rank, shape=shape, steps=args.steps, world=dist.world,
                        strong=strong, compact=args.desc)
-    r = timed_loop(engine, dist, args.steps, args.warmup)
+    use_graph = args.graph == "on" or (args.graph == "auto" and len(engine.batches) > 1)
+    graph = engine.capture(args.steps) if use_graph else None
+    ramp_steps = clock_ramp(engine, args.ramp_s, graph=graph) if args.ramp_s > 0 else 0
+    r = timed_loop(engine, dist, args.steps, args.warmup, graph=graph)
     elapsed = r["elapsed_s"]
     # all ranks' payload (strong: the shards add up to the config's one batch)
     step_bytes = int(dist.sum(engine.payload_bytes))
@@ -474,6 +533,7 @@ def main(argv=None):
         "n_gpus": dist.world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "clock_ramp": {"seconds": args.ramp_s, "untimed_launches": ramp_steps * (args.steps if graph else 1)},
         "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
@@ -493,6 +553,8 @@ def main(argv=None):
                             "packed": "packed: u16 length + u16 seed per packet, u64 offset per 64 packets "
                                       "(rns_csum_batch_packed_dev)"}[engine.form],
             "rotating_batches": len(engine.batches),
+            "launch": (f"one HIP graph of the {args.steps} step launches (torch.cuda.CUDAGraph), replayed once"
+                       if use_graph else "one C-ABI call per step"),
         },
         "roofline": {
             "bound": "hbm",

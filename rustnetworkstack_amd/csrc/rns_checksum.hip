@@ -1934,7 +1934,15 @@ int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
     const dim3 grid(static_cast<uint32_t>((waves + kBlock / 64 - 1) / (kBlock / 64))), block(kBlock);
     hipStream_t st = static_cast<hipStream_t>(stream);
     // nontemporal loads for long fragments, as pick_shape chooses for packets
-    const bool nt = pick_shape(frag_len_hint ? frag_len_hint : 512u).variant & 2u;
+    // Nontemporal loads for NetBuffer-sized fragments (c3 as 3 fragments: 298 -> 289 us
+    // packed back to back, 281 -> 261 us in 512-byte buffers), not for IMIX's mix of
+    // 40-byte packets and 512-byte fragments (646 -> 670 us): profiles/r02_chain_ab.json.
+#ifdef RNS_CHAIN_NT  // A/B knob: 1 = always nontemporal, 0 = never
+    const bool nt = RNS_CHAIN_NT;
+    (void)frag_len_hint;
+#else
+    const bool nt = (frag_len_hint ? frag_len_hint : 512u) >= 384u;
+#endif
     const bool buf = buf_records(a) < kOobOffset;
 #define RNS_CHAIN_LAUNCH(KM)                                                                      \
     if (nt && buf)                                                                                \

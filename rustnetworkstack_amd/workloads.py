@@ -163,6 +163,19 @@ class DeviceBatch:
                                                 compact=compact)
         return self._prepared[key]
 
+    def rebind(self, complement: bool = False, shape=None, compact: bool = False, packed: bool = False):
+        """A fresh launcher bound to the CURRENT stream (e.g. a graph-capture stream),
+        from the descriptors launcher() already uploaded (no copies: safe inside a
+        capture).  Not cached."""
+        from .batch import PackedBatch, PreparedBatch
+        bound = self.launcher(complement, shape, compact, packed)  # uploads once, outside any capture
+        if packed:
+            return PackedBatch(self.arena, self.blk_off, self.len16, self.seed, align_log2=ALIGN.bit_length() - 1,
+                               complement=complement, out=self.out, len_hint=int(round(self.layout.mean_len)))
+        off = bound._keep[1]
+        return PreparedBatch(self.arena, off, self.length, self.seed, complement=complement, out=self.out,
+                             len_hint=int(round(self.layout.mean_len)), shape=shape, compact=compact)
+
     def run(self, complement: bool = False, shape=None):
         return self.launcher(complement, shape)()
 
