@@ -534,6 +534,9 @@ def main(argv=None):
         "steps": args.steps,
         "warmup": args.warmup,
         "clock_ramp": {"seconds": args.ramp_s, "untimed_launches": ramp_steps * (args.steps if graph else 1)},
+        # kernel launches before the first timed one (ramp + warmup; a graph warmup is one replay of K)
+        "launches_before_timed": ramp_steps * (args.steps if graph else 1)
+        + ((args.steps if args.warmup else 0) if graph else args.warmup),
         "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "higher_is_better": True,
         "scaling": "strong" if strong else "weak",

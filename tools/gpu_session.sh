@@ -47,9 +47,9 @@ if [ -z "${SKIP_PMC:-}" ]; then
   cd /tmp
   # HBM traffic: FETCH_SIZE and WRITE_SIZE in separate passes, counters only (no other trace domains)
   step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-       python3 "$ROOT/bench.py" --no-cpu-baseline --no-host-pipeline --steps 5 --warmup 1 --config "$CONFIG"
+       python3 "$ROOT/bench.py" --no-cpu-baseline --no-host-pipeline --ramp-s 0 --steps 5 --warmup 1 --config "$CONFIG"
   step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-       python3 "$ROOT/bench.py" --no-cpu-baseline --no-host-pipeline --steps 5 --warmup 1 --config "$CONFIG"
+       python3 "$ROOT/bench.py" --no-cpu-baseline --no-host-pipeline --ramp-s 0 --steps 5 --warmup 1 --config "$CONFIG"
   cd "$ROOT"
   ALGO=$(python -c "import json;print([json.loads(l) for l in open('$OUT/bench_prof.log') if l.startswith('{')][-1]['roofline']['algorithmic_bytes_per_launch'])")
   python tools/pmc_traffic.py --fetch "$OUT/pmc_fetch" --write "$OUT/pmc_write" --config "$CONFIG" \

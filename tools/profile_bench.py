@@ -37,7 +37,7 @@ def main():
 
     line = [ln for ln in open(args.bench) if ln.startswith("{")][-1]
     b = json.loads(line)
-    W, K = b["warmup"], b["steps"]
+    W, K = b.get("launches_before_timed", b["warmup"]), b["steps"]
     M = b["roofline"].get("evpair_launches", 0)
     rows = [r for r in csv.DictReader(open(args.trace)) if args.kernel in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
@@ -61,7 +61,8 @@ def main():
     gaps = [(int(mine[i + 1]["Start_Timestamp"]) - int(mine[i]["End_Timestamp"])) / 1e3 for i in range(W, W + K - 1)]
     out = {
         "command": "rocprofv3 --kernel-trace --stats --output-format csv -- python3 bench.py "
-                   f"--gpus 1 --steps {K} --warmup {W}",
+                   f"--gpus 1 --steps {K} --warmup {b['warmup']}",
+        "untimed_launches_skipped": W,
         "kernel": name,
         "grid_size_x": grid,
         "rotating_batches": rot,
