@@ -73,9 +73,12 @@ def parse_args(argv=None):
                         "~0.1 s of load and 493-496 us after it (profiles/r02_clock_ramp.json); 0 = off")
     p.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                    help="launch the K timed steps (and the warmup) as one HIP graph of K kernel launches "
-                        "(torch.cuda.CUDAGraph): no host launch cost between steps; auto = on for batches "
-                        "small enough to rotate (c2), whose ~13 us kernels the host cannot launch one by one "
-                        "fast enough")
+                        "(torch.cuda.CUDAGraph) alternating over --graph-streams streams: no host launch cost "
+                        "between steps, and consecutive (independent) batches overlap one kernel's drain with the "
+                        "next one's ramp (c2 13.5 -> 11.8 us per step, c3 -4 %%, c5 -1.5 %%, c4 -1.2 %%: "
+                        "profiles/r02_graph_overlap.json); auto = on (every rank, so N=1 and N>1 are timed alike)")
+    p.add_argument("--graph-streams", type=int, default=2,
+                   help="graph mode: steps alternate over this many streams (independent batches may overlap)")
     p.add_argument("--scaling", choices=("auto", "weak", "strong"), default="auto",
                    help="weak: every rank checksums a full batch of the config; strong: the config's batch is "
                         "sharded by packet index across ranks (auto: strong for c5_imix, whose BASELINE.json "
@@ -303,19 +306,31 @@ class GpuEngine:
         b.launcher(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)()  # one ctypes call
         self.last = b
 
-    def capture(self, steps: int):
+    def capture(self, steps: int, streams: int = 1):
         """K steps captured as one HIP graph (K kernel launches, rotating batches in
-        step order), each launcher re-bound to the capture stream."""
+        step order), each launcher re-bound to its capture stream.  streams > 1: step
+        i goes to stream i % streams (forked from and joined back to the capture
+        stream), so consecutive steps — independent batches — may overlap on the
+        device: one kernel's ramp-up under the previous one's drain."""
         torch = self.torch
         fns = [b.rebind(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)
                for b in self.batches]
         del fns  # (bound once outside the capture: descriptor uploads happen here, not inside it)
+        side = [torch.cuda.Stream(device=self.device) for _ in range(max(streams, 1) - 1)]
         self.sync()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread_local: a process group's watchdog thread may query events while this thread captures
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            cap = torch.cuda.current_stream()
+            for s_ in side:
+                s_.wait_stream(cap)
+            lanes = [cap] + side
             for i in range(steps):
                 b = self.batches[i % len(self.batches)]
-                b.rebind(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)()
+                with torch.cuda.stream(lanes[i % len(lanes)]):
+                    b.rebind(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)()
+            for s_ in side:
+                cap.wait_stream(s_)
         self.sync()
         self.last = self.batches[(steps - 1) % len(self.batches)]
         return g
@@ -492,6 +507,17 @@ def host_pipeline_rate(engine: GpuEngine) -> dict:
             "matches_device_resident": exact}
 
 
+class _NoDist:
+    """Single-process stand-in for Dist (the isolated re-measurement needs no barrier)."""
+    enabled = False
+
+    def barrier(self):
+        pass
+
+    def max(self, x):
+        return x
+
+
 def load_traffic(path: str, config: str):
     path = path.format(config=config)
     if not os.path.exists(path):
@@ -508,8 +534,8 @@ def main(argv=None):
     strong = args.scaling == "strong" or (args.scaling == "auto" and args.config == "c5_imix")
     engine = GpuEngine(args.config, dist.rank, dist.local_rank, shape=shape, steps=args.steps, world=dist.world,
                        strong=strong, compact=args.desc)
-    use_graph = args.graph == "on" or (args.graph == "auto" and len(engine.batches) > 1)
-    graph = engine.capture(args.steps) if use_graph else None
+    use_graph = args.graph == "on" or (args.graph == "auto" and engine.device.type == "cuda")
+    graph = engine.capture(args.steps, args.graph_streams) if use_graph else None
     ramp_steps = clock_ramp(engine, args.ramp_s, graph=graph) if args.ramp_s > 0 else 0
     r = timed_loop(engine, dist, args.steps, args.warmup, graph=graph)
     elapsed = r["elapsed_s"]
@@ -518,6 +544,13 @@ def main(argv=None):
     total_bytes = step_bytes * args.steps
     value = total_bytes / elapsed / 2 ** 30
     kernel_ms = r["kernel_ms"]
+    isolated = None
+    if use_graph and args.graph_streams > 1:
+        # the same K launches one after another on ONE stream, as a graph too (no host launch cost;
+        # untimed for `value`): the per-dispatch duration rocprof reports, next to the pipelined
+        # per-step time above
+        ri = timed_loop(engine, _NoDist(), args.steps, 0, graph=engine.capture(args.steps, 1))
+        isolated = ri["kernel_ms"] * 1e3
     per = engine.per_launch_us(args.median_launches) if args.median_launches > 0 else []
     algo_bytes = engine.payload_bytes + 2 * engine.n
     # descriptor bytes a launch reads (seeds included): packed 2 B length + 8 B per 64 packets
@@ -556,8 +589,8 @@ def main(argv=None):
                             "packed": "packed: u16 length + u16 seed per packet, u64 offset per 64 packets "
                                       "(rns_csum_batch_packed_dev)"}[engine.form],
             "rotating_batches": len(engine.batches),
-            "launch": (f"one HIP graph of the {args.steps} step launches (torch.cuda.CUDAGraph), replayed once"
-                       if use_graph else "one C-ABI call per step"),
+            "launch": (f"one HIP graph of the {args.steps} step launches (torch.cuda.CUDAGraph) over "
+                       f"{args.graph_streams} stream(s), replayed once" if use_graph else "one C-ABI call per step"),
         },
         "roofline": {
             "bound": "hbm",
@@ -568,7 +601,11 @@ def main(argv=None):
             "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
             "kernel": engine.kernel_name() if shape is None else f"shape {list(shape)}",
             "kernel_avg_us": round(kernel_us, 2),
-            "frac_from": "kernel_avg_us: one event pair (launch stream) around the K back-to-back timed launches / K",
+            "frac_from": ("kernel_avg_us: one event pair (capture stream) around the graph replay of the K timed "
+                          "launches / K — consecutive steps overlap on " + str(args.graph_streams) + " streams, so "
+                          "this is the per-step time, shorter than one dispatch (isolated below)"
+                          if isolated is not None else
+                          "kernel_avg_us: one event pair (launch stream) around the K back-to-back timed launches / K"),
             "algorithmic_bytes_per_launch": algo_bytes,
             "descriptor_bytes_per_launch": desc_bytes,
             "frac_incl_descriptors": round((algo_bytes + desc_bytes) / (kernel_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
@@ -576,6 +613,13 @@ def main(argv=None):
         },
         "cpu_baseline": None,
     }
+    if isolated is not None:
+        line["roofline"]["isolated"] = {
+            "kernel_avg_us": round(isolated, 2),
+            "frac": round(algo_bytes / (isolated * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "launches": args.steps,
+            "how": "after the timed region: the same K launches as a graph on ONE stream (no overlap), one event "
+                   "pair / K (what rocprof's per-dispatch durations measure)"}
     if per:
         srt = sorted(per)
         line["roofline"]["evpair_median_us"] = round(srt[len(srt) // 2], 2)

@@ -352,7 +352,19 @@ struct Pkt {
     bool big;             // > kNoWrapBytes: exact big-endian path
     int stash_lo;         // stash: first chunk to copy to LDS
     int stash_at;         // stash: LDS chunk index of that chunk's slot
+    uint32_t len;         // in-round fill (RNS_FILL_INROUND): the packet's length,
+    uint32_t aux;         //   its checksum field offset
+    uint32_t seed;        //   and its seed
 };
+
+// A/B knob: transmit fill stores each packet's field from the group that summed it,
+// in the same round (the block's lines were just read), instead of from the owner
+// lane after the wave's 64 packets.
+#ifdef RNS_FILL_INROUND
+constexpr bool kFillInRound = true;
+#else
+constexpr bool kFillInRound = false;
+#endif
 
 __device__ __forceinline__ Pkt make_pkt(uint64_t start, uint32_t L)
 {
@@ -365,6 +377,9 @@ __device__ __forceinline__ Pkt make_pkt(uint64_t start, uint32_t L)
     k.big = L > kNoWrapBytes;
     k.stash_lo = 0;
     k.stash_at = 0;
+    k.len = L;
+    k.aux = 0xFFFFFFFFu;
+    k.seed = 0;
     return k;
 }
 
@@ -386,7 +401,7 @@ __device__ __forceinline__ void set_stash(Pkt &k, uint32_t slot, uint32_t field,
 
 template <int G, int MODE = kStashNone>
 __device__ __forceinline__ Pkt fetch_pkt(uint64_t d_start, uint32_t d_len, uint32_t src, uint32_t d_aux = 0xFFFFFFFFu,
-                                         uint32_t apar = 0)
+                                         uint32_t apar = 0, uint32_t d_seed = 0)
 {
     const uint32_t lo = bcast_from<G>(static_cast<uint32_t>(d_start), src);
     const uint32_t hi = bcast_from<G>(static_cast<uint32_t>(d_start >> 32), src);
@@ -394,6 +409,10 @@ __device__ __forceinline__ Pkt fetch_pkt(uint64_t d_start, uint32_t d_len, uint3
     const uint32_t x = MODE == kStashField ? bcast_from<G>(d_aux, src) : 0xFFFFFFFFu;
     Pkt k = make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L);
     set_stash<MODE>(k, src, x, apar);
+    if constexpr (MODE == kStashField && kFillInRound) {
+        k.aux = x;
+        k.seed = bcast_from<G>(d_seed, src);
+    }
     return k;
 }
 
@@ -735,7 +754,7 @@ constexpr int kUMax = 4;
 template <bool NT, bool BUF, int MODE>
 __device__ __forceinline__ Pkt prefetch_class(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint32_t n,
                                               const ClassRun (&cr)[kNumClasses], uint64_t s_start, uint32_t s_len,
-                                              uint32_t s_aux, uint32_t lane, uint4 (&w)[kUMax])
+                                              uint32_t s_aux, uint32_t lane, uint4 (&w)[kUMax], uint32_t s_seed = 0)
 {
     uint32_t lg = 6, U = 0, off = 0, cnt = 0;
 #pragma unroll
@@ -757,6 +776,10 @@ __device__ __forceinline__ Pkt prefetch_class(const CsumArgs &a, __amdgpu_buffer
     const uint32_t x = MODE == kStashField ? static_cast<uint32_t>(__shfl(static_cast<int>(s_aux), src, 64)) : 0xFFFFFFFFu;
     Pkt k = make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L);
     set_stash<MODE>(k, static_cast<uint32_t>(src), x, arena_parity(a));
+    if constexpr (MODE == kStashField && kFillInRound) {
+        k.aux = x;
+        k.seed = static_cast<uint32_t>(__shfl(static_cast<int>(s_seed), src, 64));
+    }
     k.nch = valid ? k.nch : 0u;
     const uint64_t first = k.start - static_cast<uint64_t>(k.s);
 #pragma unroll
@@ -775,13 +798,88 @@ __device__ __forceinline__ Pkt prefetch_class(const CsumArgs &a, __amdgpu_buffer
     return k;
 }
 
+// Transmit fill (kStashField): where the field's bytes sit in the stashed block, their
+// word contribution (they count as zero, buf.rs:286-288), and the largest aligned
+// block around the field that lies inside the packet (rewritten whole: no partial-
+// sector write).  sb = the packet's stash; the block starts at stash chunk 0.
+struct FillSite {
+    uint64_t blk;      // offset (from a.arena) of the stashed block around the field
+    uint32_t f_rel;    // the field's first byte in that block (0 .. kFieldBlock-1)
+    uint32_t w_size;   // bytes of the largest aligned block inside the packet (0: none)
+    uint32_t contrib;  // the field's two bytes as the packet's word sum holds them
+};
+
+__device__ __forceinline__ FillSite fill_site(const CsumArgs &a, uint64_t d_start, uint32_t d_len, uint32_t d_field,
+                                              bool big, const uint8_t *sb, bool ok)
+{
+    FillSite f;
+    const uint32_t s = static_cast<uint32_t>(d_start & 15);
+    const uint32_t fpos = s + d_field;  // from chunk 0's first byte
+    const int lo = field_block_lo(fpos >> 4, static_cast<uint32_t>(d_start >> 4), arena_parity(a));
+    f.f_rel = fpos - 16u * static_cast<uint32_t>(lo);
+    f.blk = d_start - s + static_cast<uint64_t>(16 * static_cast<int64_t>(lo));
+    const uint32_t b0 = ok ? sb[f.f_rel] : 0u, b1 = ok ? sb[f.f_rel + 1] : 0u;
+    // LE words pair aligned bytes; the exact BE path pairs from the packet start
+    const bool hi_first = big ? !(d_field & 1) : (fpos & 1);
+    f.contrib = hi_first ? (b0 << 8) + b1 : b0 + (b1 << 8);
+    f.w_size = 0;
+#pragma unroll
+    for (uint32_t bs = 32; bs <= static_cast<uint32_t>(kFieldBlock); bs *= 2) {
+        const uint64_t b = f.blk + (f.f_rel & ~(bs - 1));  // the bs-byte block holding the field
+        const bool in = lo >= 0 && b >= d_start && b + bs <= d_start + d_len && (f.f_rel & (bs - 1)) != bs - 1;
+        f.w_size = in ? bs : f.w_size;
+    }
+    return f;
+}
+
+// set_be16(&mut header[f..f+2], checksum): rewrite the block from the stash (stp =
+// the packet's stash chunks) with the field patched in, or store the two bytes.
+__device__ __forceinline__ void fill_store(const CsumArgs &a, const FillSite &f, uint64_t d_start, uint32_t d_field,
+                                           uint16_t res, const uint4 *stp)
+{
+#ifndef RNS_FILL_NOSTORE
+    uint8_t *arena_w = const_cast<uint8_t *>(a.arena);
+    const uint32_t be = (res >> 8) | ((res & 0xffu) << 8);
+    if (f.w_size) {
+        // The whole block belongs to this packet (packets never overlap) and its
+        // bytes are in the stash: rewrite it entirely, since a full-sector write
+        // needs no read-modify-write at the memory side.
+        const uint32_t c_lo = (f.f_rel & ~(f.w_size - 1)) >> 4, c_hi = c_lo + (f.w_size >> 4);
+#pragma unroll
+        for (uint32_t i = 0; i < static_cast<uint32_t>(kFieldChunks); ++i) {
+            if (i >= c_lo && i < c_hi) {
+                const uint4 c = stp[i];
+                uint32_t w[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+                for (uint32_t k = 0; k < 2; ++k) {  // bytes f_rel and f_rel+1
+                    const uint32_t bpos = f.f_rel + k - 16 * i, sh = (bpos & 3) * 8;
+                    const uint32_t byte = (be >> (8 * k)) & 0xffu;
+#pragma unroll
+                    for (uint32_t d = 0; d < 4; ++d)
+                        if (bpos < 16 && d == (bpos >> 2))
+                            w[d] = (w[d] & ~(0xffu << sh)) | (byte << sh);
+                }
+                *reinterpret_cast<uint4 *>(arena_w + f.blk + 16 * i) = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+    } else {
+        uint8_t *q = arena_w + d_start + d_field;
+        q[0] = static_cast<uint8_t>(res >> 8);
+        q[1] = static_cast<uint8_t>(res);
+    }
+#else
+    (void)a; (void)f; (void)d_start; (void)d_field; (void)res; (void)stp;
+#endif
+}
+
 // All rounds of class C.  On entry (cur, v) hold round 0's prefetched first pass;
 // on exit they hold the first pass of class `next` (the next non-empty class).
 template <uint32_t C, bool NT, bool BUF, int MODE>
 __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc,
                                           const ClassRun (&cr)[kNumClasses], uint32_t next, uint64_t s_start,
                                           uint32_t s_len, uint32_t s_aux, bool in_class, uint32_t rank,
-                                          uint32_t lane, Pkt &cur, uint4 (&v)[kUMax], uint32_t &mine, uint4 *st)
+                                          uint32_t lane, Pkt &cur, uint4 (&v)[kUMax], uint32_t &mine, uint4 *st,
+                                          uint32_t s_seed)
 {
     constexpr int G = 1 << kClassLog2G[C];
     constexpr int U = static_cast<int>(kClassU[C]);
@@ -793,13 +891,26 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
         return;  // (cur, v) already hold the next class's prefetch
     auto fetch = [&](uint32_t r) {  // group `grp` of round r: sorted position off + r*P + grp
         const uint32_t i = r * P + grp;
-        Pkt k = fetch_pkt<G, MODE>(s_start, s_len, cr[C].off + (i < cr[C].cnt ? i : 0), s_aux, arena_parity(a));
+        Pkt k = fetch_pkt<G, MODE>(s_start, s_len, cr[C].off + (i < cr[C].cnt ? i : 0), s_aux, arena_parity(a),
+                                   s_seed);
         k.nch = (i < cr[C].cnt) ? k.nch : 0u;
         return k;
     };
     auto finish = [&](uint32_t r) {  // consume round r from (cur, v), route each sum to its owner lane
-        const uint32_t words =
-            group_allreduce<G>(packet_partial<G, U, NT, BUF, kUMax, MODE>(a, rsrc, cur, sub, v, st));
+        uint32_t words = group_allreduce<G>(packet_partial<G, U, NT, BUF, kUMax, MODE>(a, rsrc, cur, sub, v, st));
+        if constexpr (MODE == kStashField && kFillInRound) {
+            // the group finishes its packet now, while the field's lines were just read:
+            // words -> the complemented result, stored into the field by lane 0 of the group
+            wave_lds_fence();  // the stash was written by this group's lanes
+            const bool ok = cur.nch != 0;  // a rejected packet was given length 0
+            const uint4 *stp = st + cur.stash_at;
+            const FillSite f = fill_site(a, cur.start, cur.len, cur.aux, cur.big,
+                                         reinterpret_cast<const uint8_t *>(stp), ok);
+            const uint16_t res = finalize_bits(words - f.contrib, cur.start & 1, cur.big, cur.seed, ok, a.flags);
+            if (ok && sub == 0)
+                fill_store(a, f, cur.start, cur.aux, res, stp);
+            words = res;
+        }
         if constexpr (G == 64) {
             mine = (in_class && rank == r) ? words : mine;  // wave-uniform sum
         } else {
@@ -819,7 +930,7 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
             v[u] = w[u];
     }
     uint4 w[kUMax];
-    const Pkt nxt = prefetch_class<NT, BUF, MODE>(a, rsrc, next, cr, s_start, s_len, s_aux, lane, w);
+    const Pkt nxt = prefetch_class<NT, BUF, MODE>(a, rsrc, next, cr, s_start, s_len, s_aux, lane, w, s_seed);
     finish(rounds - 1);
     cur = nxt;
 #pragma unroll
@@ -837,7 +948,7 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
 template <bool NT, bool BUF, int MODE>
 __device__ __forceinline__ uint32_t wave_class_pass(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint64_t d_start,
                                                     uint32_t d_len, uint32_t d_aux, uint32_t lane, uint4 *st,
-                                                    uint32_t &pos)
+                                                    uint32_t &pos, uint32_t d_seed = 0)
 {
     // size class of this lane's packet; ranks within the class; sorted position
     const uint32_t nch = d_len ? static_cast<uint32_t>(((d_start & 15) + d_len + 15) >> 4) : 0u;
@@ -876,13 +987,15 @@ __device__ __forceinline__ uint32_t wave_class_pass(const CsumArgs &a, __amdgpu_
     const uint64_t s_start = (static_cast<uint64_t>(s_hi) << 32) | s_lo;
     const uint32_t s_aux = MODE == kStashField
         ? static_cast<uint32_t>(__builtin_amdgcn_ds_permute(addr, static_cast<int>(d_aux))) : 0u;
+    const uint32_t s_seed = (MODE == kStashField && kFillInRound)
+        ? static_cast<uint32_t>(__builtin_amdgcn_ds_permute(addr, static_cast<int>(d_seed))) : 0u;
 
     uint32_t mine = 0;
     uint4 v[kUMax];
-    Pkt cur = prefetch_class<NT, BUF, MODE>(a, rsrc, next[0], cr, s_start, s_len, s_aux, lane, v);
+    Pkt cur = prefetch_class<NT, BUF, MODE>(a, rsrc, next[0], cr, s_start, s_len, s_aux, lane, v, s_seed);
 #define RNS_RUN_CLASS(C)                                                                                  \
     run_class<C, NT, BUF, MODE>(a, rsrc, cr, next[C + 1], s_start, s_len, s_aux, cls == C, rank, lane, \
-                                cur, v, mine, st)
+                                cur, v, mine, st, s_seed)
     RNS_RUN_CLASS(0);
     RNS_RUN_CLASS(1);
     RNS_RUN_CLASS(2);
@@ -1147,7 +1260,7 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX
         }
         const bool odd = d_start & 1, big = d_len > kNoWrapBytes;  // all finalize needs of (start, len)
         uint32_t pos;
-        uint32_t mine = wave_class_pass<NT, BUF, kMode>(a, rsrc, d_start, d_len, d_field, lane, st, pos);
+        uint32_t mine = wave_class_pass<NT, BUF, kMode>(a, rsrc, d_start, d_len, d_field, lane, st, pos, d_seed);
 
         if constexpr (TX) {
             // Transmit finalize: mine = the whole datagram's word sum.  From the stash
@@ -1302,67 +1415,24 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX
             }
             continue;
         }
-        uint64_t blk = 0;      // FILL: offset (from a.arena) of the stashed block around the field
-        uint32_t f_rel = 0;    // FILL: the field's first byte in that block (0 .. kFieldBlock-1)
-        uint32_t w_size = 0;   // FILL: bytes of the largest aligned block inside the packet (0: none)
-        if constexpr (FILL) {  // take the field's bytes out of the sum: it counts as zero
-            const uint32_t s = static_cast<uint32_t>(d_start & 15);
-            const uint32_t fpos = s + d_field;                       // from chunk 0's first byte
-            const int lo = field_block_lo(fpos >> 4, static_cast<uint32_t>(d_start >> 4), arena_parity(a));
-            f_rel = fpos - 16u * static_cast<uint32_t>(lo);
-            blk = d_start - s + static_cast<uint64_t>(16 * static_cast<int64_t>(lo));
+        FillSite fs{};
+        if constexpr (FILL && !kFillInRound) {  // take the field's bytes out of the sum: it counts as zero
             wave_lds_fence();  // the stash was written by other lanes of this wave
-            const uint8_t *sb = reinterpret_cast<const uint8_t *>(st + pos * kNS);
-            const uint32_t b0 = d_ok ? sb[f_rel] : 0u, b1 = d_ok ? sb[f_rel + 1] : 0u;
-            // LE words pair aligned bytes; the exact BE path pairs from the packet start
-            const bool hi_first = big ? !(d_field & 1) : (fpos & 1);
-            mine -= hi_first ? (b0 << 8) + b1 : b0 + (b1 << 8);
-#pragma unroll
-            for (uint32_t bs = 32; bs <= static_cast<uint32_t>(kFieldBlock); bs *= 2) {
-                const uint64_t b = blk + (f_rel & ~(bs - 1));       // the bs-byte block holding the field
-                const bool in = lo >= 0 && b >= d_start && b + bs <= d_start + d_len && (f_rel & (bs - 1)) != bs - 1;
-                w_size = in ? bs : w_size;
-            }
+            fs = fill_site(a, d_start, d_len, d_field, big, reinterpret_cast<const uint8_t *>(st + pos * kNS), d_ok);
+            mine -= fs.contrib;
         }
         if constexpr (PACKED)
             d_seed = (a.seed && live) ? a.seed[p] : 0u;
-        const uint16_t res = finalize_bits(mine, odd, big, d_seed, d_ok, a.flags);
+        uint16_t res;
+        if constexpr (FILL && kFillInRound)
+            res = d_ok ? static_cast<uint16_t>(mine) : static_cast<uint16_t>(0);  // finished (and stored) in-round
+        else
+            res = finalize_bits(mine, odd, big, d_seed, d_ok, a.flags);
         if (live && a.out)
             a.out[p] = res;  // 64 consecutive u16: one 128-byte store
-        if constexpr (FILL) {
-#ifndef RNS_FILL_NOSTORE
-            if (live && d_ok) {  // set_be16(&mut header[f..f+2], checksum)
-                uint8_t *arena_w = const_cast<uint8_t *>(a.arena);
-                const uint32_t be = (res >> 8) | ((res & 0xffu) << 8);
-                if (w_size) {
-                    // The whole block belongs to this packet (packets never overlap) and its
-                    // bytes are in the stash: rewrite it entirely, since a full-sector write
-                    // needs no read-modify-write at the memory side.
-                    const uint32_t c_lo = (f_rel & ~(w_size - 1)) >> 4, c_hi = c_lo + (w_size >> 4);
-#pragma unroll
-                    for (uint32_t i = 0; i < static_cast<uint32_t>(kFieldChunks); ++i) {
-                        if (i >= c_lo && i < c_hi) {
-                            const uint4 c = st[pos * kNS + i];
-                            uint32_t w[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-                            for (uint32_t k = 0; k < 2; ++k) {  // bytes f_rel and f_rel+1
-                                const uint32_t bpos = f_rel + k - 16 * i, sh = (bpos & 3) * 8;
-                                const uint32_t byte = (be >> (8 * k)) & 0xffu;
-#pragma unroll
-                                for (uint32_t d = 0; d < 4; ++d)
-                                    if (bpos < 16 && d == (bpos >> 2))
-                                        w[d] = (w[d] & ~(0xffu << sh)) | (byte << sh);
-                            }
-                            *reinterpret_cast<uint4 *>(arena_w + blk + 16 * i) = make_uint4(w[0], w[1], w[2], w[3]);
-                        }
-                    }
-                } else {
-                    uint8_t *q = arena_w + d_start + d_field;
-                    q[0] = static_cast<uint8_t>(res >> 8);
-                    q[1] = static_cast<uint8_t>(res);
-                }
-            }
-#endif
+        if constexpr (FILL && !kFillInRound) {
+            if (live && d_ok)  // set_be16(&mut header[f..f+2], checksum), after the wave read its 64 packets
+                fill_store(a, fs, d_start, d_field, res, st + pos * kNS);
         }
         if (a.bad) {
             const uint64_t rejected = __ballot(live && !d_ok);

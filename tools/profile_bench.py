@@ -47,11 +47,13 @@ def main():
     name = rows[0]["Kernel_Name"]
     mine = [r for r in rows if int(r["Grid_Size_X"]) == grid and r["Kernel_Name"] == name]
     rot = b["config"].get("rotating_batches", 1)
-    need = W + K + M
+    iso = b["roofline"].get("isolated")
+    n_iso = iso["launches"] if iso else 0
+    need = W + K + n_iso + M
     if len(mine) < need:
         raise SystemExit(f"trace has {len(mine)} dispatches of the bench kernel, expected >= {need}")
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in mine[:need]]
-    timed, per = dur[W:W + K], dur[W + K:need]
+    timed, iso_d, per = dur[W:W + K], dur[W + K:W + K + n_iso], dur[W + K + n_iso:need]
     algo = b["roofline"]["algorithmic_bytes_per_launch"]
     peak = b["roofline"]["peak"]
 
@@ -59,6 +61,11 @@ def main():
         return round(algo / (us * 1e-6) / 1e9 / peak, 4)
 
     gaps = [(int(mine[i + 1]["Start_Timestamp"]) - int(mine[i]["End_Timestamp"])) / 1e3 for i in range(W, W + K - 1)]
+    # span of the K timed dispatches (first start to last end) / K: the per-step time when
+    # consecutive steps overlap on several streams (bench.py graph mode)
+    span = (max(int(r["End_Timestamp"]) for r in mine[W:W + K]) -
+            min(int(r["Start_Timestamp"]) for r in mine[W:W + K])) / 1e3 / K
+
     out = {
         "command": "rocprofv3 --kernel-trace --stats --output-format csv -- python3 bench.py "
                    f"--gpus 1 --steps {K} --warmup {b['warmup']}",
@@ -75,9 +82,18 @@ def main():
                                                   "max": round(max(gaps), 2) if gaps else None},
         "bench": {"kernel_avg_us": b["roofline"]["kernel_avg_us"], "evpair_median_us": b["roofline"].get("evpair_median_us"),
                   "frac": b["roofline"]["frac"], "value": b["value"], "ms_per_step": b["ms_per_step"]},
+        "rocprof_timed_span_us_per_launch": round(span, 2),
+        "frac_from_rocprof_timed_span": frac(span),
         "frac_from_rocprof_timed_median": frac(statistics.median(timed)),
         "bench_frac_vs_rocprof_timed_median": round(b["roofline"]["frac"] / frac(statistics.median(timed)) - 1, 4),
+        "bench_frac_vs_rocprof_timed_span": round(b["roofline"]["frac"] / frac(span) - 1, 4),
     }
+    if iso_d:
+        out["isolated"] = {"bench_kernel_avg_us": iso["kernel_avg_us"], "bench_frac": iso["frac"],
+                           "rocprof_per_dispatch_us": {"mean": round(statistics.mean(iso_d), 2),
+                                                       "median": round(statistics.median(iso_d), 2)},
+                           "frac_from_rocprof_median": frac(statistics.median(iso_d)),
+                           "bench_vs_rocprof_median": round(iso["frac"] / frac(statistics.median(iso_d)) - 1, 4)}
     if args.stats:
         out["stats_csv"] = [r for r in csv.DictReader(open(args.stats))]
         out["stats_csv_note"] = ("whole-run --stats: the product kernel's row also counts the warmup launches and "
@@ -92,8 +108,9 @@ def main():
                         max(ns), round(statistics.pstdev(ns), 3)])
     with open(args.out, "w") as f:
         json.dump(out, f, indent=1)
-    print(json.dumps({k: out[k] for k in ("rocprof_timed_us", "rocprof_evpair_launches_us", "bench",
-                                          "frac_from_rocprof_timed_median", "bench_frac_vs_rocprof_timed_median")}))
+    print(json.dumps({k: out.get(k) for k in ("rocprof_timed_us", "rocprof_timed_span_us_per_launch", "bench",
+                                              "frac_from_rocprof_timed_span", "bench_frac_vs_rocprof_timed_span",
+                                              "frac_from_rocprof_timed_median", "isolated")}))
 
 
 if __name__ == "__main__":
