@@ -77,8 +77,11 @@ def parse_args(argv=None):
                         "between steps, and consecutive (independent) batches overlap one kernel's drain with the "
                         "next one's ramp (c2 13.5 -> 11.8 us per step, c3 -4 %%, c5 -1.5 %%, c4 -1.2 %%: "
                         "profiles/r02_graph_overlap.json); auto = on (every rank, so N=1 and N>1 are timed alike)")
-    p.add_argument("--graph-streams", type=int, default=2,
-                   help="graph mode: steps alternate over this many streams (independent batches may overlap)")
+    p.add_argument("--graph-streams", type=int, default=0,
+                   help="graph mode: steps alternate over this many streams (independent batches may overlap); "
+                        "0 = auto: 3 for batches of small packets (mean < 1000 B: c2 11.35 -> 11.10 us, IMIX "
+                        "493 -> 481-486 us), 2 otherwise (c3: 229.5 with 2, 231-232 with 3; profiles/"
+                        "r02_graph_overlap.json)")
     p.add_argument("--scaling", choices=("auto", "weak", "strong"), default="auto",
                    help="weak: every rank checksums a full batch of the config; strong: the config's batch is "
                         "sharded by packet index across ranks (auto: strong for c5_imix, whose BASELINE.json "
@@ -535,6 +538,8 @@ def main(argv=None):
     engine = GpuEngine(args.config, dist.rank, dist.local_rank, shape=shape, steps=args.steps, world=dist.world,
                        strong=strong, compact=args.desc)
     use_graph = args.graph == "on" or (args.graph == "auto" and engine.device.type == "cuda")
+    if args.graph_streams <= 0:
+        args.graph_streams = 3 if engine.layout.mean_len < 1000 else 2
     graph = engine.capture(args.steps, args.graph_streams) if use_graph else None
     ramp_steps = clock_ramp(engine, args.ramp_s, graph=graph) if args.ramp_s > 0 else 0
     r = timed_loop(engine, dist, args.steps, args.warmup, graph=graph)
