@@ -746,7 +746,11 @@ static_assert(kNumClasses <= 6, "at most 6 size classes");
 constexpr const uint32_t (&kClassMax)[kNumClasses - 1] = kClassMaxList;
 constexpr uint32_t kClassLog2G[kNumClasses] = {RNS_CLASS_LOG2G};   // lanes per packet 4, 4, 16, 32, 64
 constexpr uint32_t kClassU[kNumClasses] = {RNS_CLASS_U};           // chunks in flight per lane
-constexpr int kUMax = 4;
+constexpr int umax_of(int i = 0, int m = 1)
+{
+    return i == static_cast<int>(kNumClasses) ? m : umax_of(i + 1, m > static_cast<int>(kClassU[i]) ? m : static_cast<int>(kClassU[i]));
+}
+constexpr int kUMax = umax_of();  // chunk slots of the widest class
 
 // Round 0 of class n (wave-uniform; kNumClasses = none), issued with the class's
 // runtime shape into the shared buffer: the last round of the previous class
@@ -938,6 +942,81 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
         v[u] = w[u];
 }
 
+// The tiny class (<= 4 chunks: IMIX's 40-byte packets, TCP ACKs) in rounds of 64
+// packets instead of 16: a group of 4 lanes takes FOUR packets per round, one per
+// chunk slot (slot q of group g = the class's packet r*64 + q*16 + g; lane `sub`
+// loads chunk `sub` of each), so the class's whole share of a wave batch is one
+// memory round (IMIX: ~37 of 64 packets; G4/U1 took 3).  Each slot is reduced in
+// its group; lane 4g + q keeps slot q's sum, and each owner lane pulls its packet's
+// with one shuffle.  Issues its own round 0 (it is always the first class) and, like
+// run_class, leaves the next class's first pass in flight in (cur, v).
+#ifndef RNS_TINY_Q
+#define RNS_TINY_Q 4
+#endif
+constexpr uint32_t kTinyQ = kFillInRound ? 1u : RNS_TINY_Q;  // 1: class 0 runs G4/U1 through run_class
+static_assert(kTinyQ == 1 || (kTinyQ == 4 && kClassLog2G[0] == 2 && kClassMax[0] <= 4), "tiny class shape");
+
+template <bool NT, bool BUF, int MODE>
+__device__ __forceinline__ void run_tiny(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc,
+                                         const ClassRun (&cr)[kNumClasses], uint32_t next, uint64_t s_start,
+                                         uint32_t s_len, uint32_t s_aux, bool in_class, uint32_t rank, uint32_t lane,
+                                         Pkt &cur, uint4 (&v)[kUMax], uint32_t &mine, uint4 *st)
+{
+    // A class pass covers 64 descriptors, so the class is ONE round (cnt <= 64).
+    constexpr int G = 4, Q = 4;
+    const uint32_t sub = lane & (G - 1);
+    const uint32_t grp = lane / G;
+    const uint32_t cnt = cr[0].cnt;
+    // per slot: the bytes of this lane's chunk that lie inside the packet, lo | hi << 8;
+    // the stash modes also keep the packet (its stash slots)
+    uint32_t bnd[Q];
+    Pkt k[MODE != kStashNone ? Q : 1];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const uint32_t i = q * 16 + grp;
+        Pkt kq = fetch_pkt<G, MODE>(s_start, s_len, cr[0].off + (i < cnt ? i : 0), s_aux, arena_parity(a));
+        kq.nch = (i < cnt) ? kq.nch : 0u;
+        uint4 one[1];
+        issue_pass<G, 1, NT, BUF, 1>(a, rsrc, kq, sub, one);
+        v[q] = one[0];
+        const uint32_t lo = sub == 0 ? static_cast<uint32_t>(kq.s) : 0u;
+        const uint32_t hi = sub + 1 == kq.nch ? static_cast<uint32_t>(kq.e) : 16u;
+        bnd[q] = sub < kq.nch ? (lo | (hi << 8)) : (16u << 8);  // absent chunks already read as zeros
+        if constexpr (MODE != kStashNone)
+            k[q] = kq;
+    }
+    uint4 w[kUMax];
+    cur = prefetch_class<NT, BUF, MODE>(a, rsrc, next, cr, s_start, s_len, s_aux, lane, w);  // next class in flight
+    uint32_t sel = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        uint4 x = v[q];
+        const int lo = static_cast<int>(bnd[q] & 0xffu), hi = static_cast<int>(bnd[q] >> 8);
+        if (lo != 0 || hi != 16) {
+            x.x = keep_bytes(x.x, lo, hi, 0);
+            x.y = keep_bytes(x.y, lo, hi, 4);
+            x.z = keep_bytes(x.z, lo, hi, 8);
+            x.w = keep_bytes(x.w, lo, hi, 12);
+        }
+        if constexpr (MODE != kStashNone) {
+            const uint4 one[1] = {x};
+            stash_chunks<MODE, G, 1, 1>(k[q], sub, one, st);
+        }
+        uint32_t s = __builtin_amdgcn_sad_u16(x.x, 0, 0u);  // <= 64 bytes: never the BE path
+        s = __builtin_amdgcn_sad_u16(x.y, 0, s);
+        s = __builtin_amdgcn_sad_u16(x.z, 0, s);
+        s = __builtin_amdgcn_sad_u16(x.w, 0, s);
+        const uint32_t words = group_allreduce<G>(s);
+        sel = (sub == static_cast<uint32_t>(q)) ? words : sel;
+    }
+    const int src = static_cast<int>(((rank & 15u) << 2) | ((rank >> 4) & 3u));  // lane 4g + q of the owner's slot
+    const uint32_t t = static_cast<uint32_t>(__shfl(static_cast<int>(sel), src, 64));
+    mine = in_class ? t : mine;
+#pragma unroll
+    for (int u = 0; u < kUMax; ++u)
+        v[u] = w[u];
+}
+
 // The size-class data pass over one wave batch: lane l holds one descriptor
 // (d_start, d_len; d_aux = the field offset for kStashField; d_len 0 = nothing to
 // read) and receives that packet's word sum — the LE sum for packets <= 128 KiB,
@@ -992,11 +1071,17 @@ __device__ __forceinline__ uint32_t wave_class_pass(const CsumArgs &a, __amdgpu_
 
     uint32_t mine = 0;
     uint4 v[kUMax];
-    Pkt cur = prefetch_class<NT, BUF, MODE>(a, rsrc, next[0], cr, s_start, s_len, s_aux, lane, v, s_seed);
+    Pkt cur;
 #define RNS_RUN_CLASS(C)                                                                                  \
     run_class<C, NT, BUF, MODE>(a, rsrc, cr, next[C + 1], s_start, s_len, s_aux, cls == C, rank, lane, \
                                 cur, v, mine, st, s_seed)
-    RNS_RUN_CLASS(0);
+    if (kTinyQ > 1 && cr[0].cnt) {  // the tiny class issues its own first round
+        run_tiny<NT, BUF, MODE>(a, rsrc, cr, next[1], s_start, s_len, s_aux, cls == 0, rank, lane, cur, v, mine, st);
+    } else {
+        cur = prefetch_class<NT, BUF, MODE>(a, rsrc, next[0], cr, s_start, s_len, s_aux, lane, v, s_seed);
+        if (kTinyQ == 1)
+            RNS_RUN_CLASS(0);
+    }
     RNS_RUN_CLASS(1);
     RNS_RUN_CLASS(2);
     RNS_RUN_CLASS(3);
