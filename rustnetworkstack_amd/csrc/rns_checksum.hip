@@ -967,9 +967,10 @@ __device__ __forceinline__ void run_tiny(const CsumArgs &a, __amdgpu_buffer_rsrc
     const uint32_t sub = lane & (G - 1);
     const uint32_t grp = lane / G;
     const uint32_t cnt = cr[0].cnt;
-    // per slot: the bytes of this lane's chunk that lie inside the packet, lo | hi << 8;
-    // the stash modes also keep the packet (its stash slots)
-    uint32_t bnd[Q];
+    // per slot q: the bytes [lo, hi) of this lane's chunk that lie inside the packet,
+    // byte q of bnd = lo | (hi - 1) << 4 (one VGPR for all four); the stash modes also
+    // keep the packet (its stash slots)
+    uint32_t bnd = 0;
     Pkt k[MODE != kStashNone ? Q : 1];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
@@ -981,7 +982,8 @@ __device__ __forceinline__ void run_tiny(const CsumArgs &a, __amdgpu_buffer_rsrc
         v[q] = one[0];
         const uint32_t lo = sub == 0 ? static_cast<uint32_t>(kq.s) : 0u;
         const uint32_t hi = sub + 1 == kq.nch ? static_cast<uint32_t>(kq.e) : 16u;
-        bnd[q] = sub < kq.nch ? (lo | (hi << 8)) : (16u << 8);  // absent chunks already read as zeros
+        const uint32_t b = sub < kq.nch ? (lo | ((hi - 1) << 4)) : 0xF0u;  // absent chunks already read as zeros
+        bnd |= b << (8 * q);
         if constexpr (MODE != kStashNone)
             k[q] = kq;
     }
@@ -991,7 +993,7 @@ __device__ __forceinline__ void run_tiny(const CsumArgs &a, __amdgpu_buffer_rsrc
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         uint4 x = v[q];
-        const int lo = static_cast<int>(bnd[q] & 0xffu), hi = static_cast<int>(bnd[q] >> 8);
+        const int lo = static_cast<int>((bnd >> (8 * q)) & 15u), hi = static_cast<int>((bnd >> (8 * q + 4)) & 15u) + 1;
         if (lo != 0 || hi != 16) {
             x.x = keep_bytes(x.x, lo, hi, 0);
             x.y = keep_bytes(x.y, lo, hi, 4);
@@ -1024,7 +1026,7 @@ __device__ __forceinline__ void run_tiny(const CsumArgs &a, __amdgpu_buffer_rsrc
 // (ballot + mbcnt ranks, ds_permute), runs every class's rounds with its own shape,
 // and routes each sum back to its owner lane.  pos = the lane's sorted position
 // (its stash slot).
-template <bool NT, bool BUF, int MODE>
+template <bool NT, bool BUF, int MODE, bool TINY = (kTinyQ > 1)>
 __device__ __forceinline__ uint32_t wave_class_pass(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint64_t d_start,
                                                     uint32_t d_len, uint32_t d_aux, uint32_t lane, uint4 *st,
                                                     uint32_t &pos, uint32_t d_seed = 0)
@@ -1075,11 +1077,11 @@ __device__ __forceinline__ uint32_t wave_class_pass(const CsumArgs &a, __amdgpu_
 #define RNS_RUN_CLASS(C)                                                                                  \
     run_class<C, NT, BUF, MODE>(a, rsrc, cr, next[C + 1], s_start, s_len, s_aux, cls == C, rank, lane, \
                                 cur, v, mine, st, s_seed)
-    if (kTinyQ > 1 && cr[0].cnt) {  // the tiny class issues its own first round
+    if (TINY && cr[0].cnt) {  // the tiny class issues its own first round
         run_tiny<NT, BUF, MODE>(a, rsrc, cr, next[1], s_start, s_len, s_aux, cls == 0, rank, lane, cur, v, mine, st);
     } else {
         cur = prefetch_class<NT, BUF, MODE>(a, rsrc, next[0], cr, s_start, s_len, s_aux, lane, v, s_seed);
-        if (kTinyQ == 1)
+        if (!TINY)
             RNS_RUN_CLASS(0);
     }
     RNS_RUN_CLASS(1);
@@ -1559,8 +1561,20 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
 
 constexpr uint32_t kChainMaxK = 8;  // packets per lane, at most
 
+// The one-round tiny class (run_tiny) in the chain kernel's class pass: only for
+// short fragments (the temporal instantiation, mean fragment < 384 B: IMIX chains
+// 870 -> 800 us in 512-byte buffers).  With NetBuffer-sized fragments there are no
+// tiny ones, and its registers made the kernel spill (c3 chains 292 -> 321 us).
+#ifndef RNS_CHAIN_TINY
+#define RNS_CHAIN_TINY 1
+#endif
+constexpr bool kChainTiny = RNS_CHAIN_TINY && kTinyQ > 1;
+
+#ifndef RNS_CHAIN_OCC
+#define RNS_CHAIN_OCC 4
+#endif
 template <bool NT, bool BUF, uint32_t KMAX>
-__global__ __launch_bounds__(kBlock, 4) void csum_chain_kernel(const CsumArgs a)
+__global__ __launch_bounds__(kBlock, RNS_CHAIN_OCC) void csum_chain_kernel(const CsumArgs a)
 {
     // A wave owns K*64 consecutive packets (K = a.chain_k, chosen by the host from the
     // mean fragment count so the wave's fragments fill whole 64-fragment batches).
@@ -1612,7 +1626,8 @@ __global__ __launch_bounds__(kBlock, 4) void csum_chain_kernel(const CsumArgs a)
             }
             const bool big = d_len > kNoWrapBytes, odd = d_start & 1;
             uint32_t pos;
-            const uint32_t w = wave_class_pass<NT, BUF, kStashNone>(a, rsrc, d_start, d_len, 0u, lane, nullptr, pos);
+            const uint32_t w =
+                wave_class_pass<NT, BUF, kStashNone, kChainTiny && !NT>(a, rsrc, d_start, d_len, 0u, lane, nullptr, pos);
             uint32_t g = w;  // big: BE sum mod 2^32; else the folded BE sum (RFC 1071 §2(B), as finalize_bits)
             if (!big) {
                 const uint32_t x = fold16(w);

@@ -36,6 +36,7 @@ HEADLINE = "c3_1500B"
 DIAG_CONFIGS = {
     "d40B": dict(n=1 << 22, kind="fixed", length=40),
     "d576B": dict(n=1 << 21, kind="fixed", length=576),
+    "d1000B": dict(n=1 << 20, kind="fixed", length=1000),
 }
 IMIX_SIZES = (40, 576, 1500)  # 7:4:1
 
