@@ -256,12 +256,14 @@ def csum_batch_strided(arena: torch.Tensor, n: int, stride: int, length: int, *,
 def csum_chain(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch.Tensor, first: torch.Tensor,
                seed: torch.Tensor | None = None, *, complement: bool = False, out: torch.Tensor | None = None,
                frag_sums: torch.Tensor | None = None, bad: torch.Tensor | None = None,
-               frag_len_hint: int = 512) -> torch.Tensor:
+               frag_len_hint: int = 512, runs: bool = False) -> torch.Tensor:
     """util.rs:112 ``compute_buffer_ones_comp`` for a batch of fragment chains.
 
     Packet i = fragments ``first[i] .. first[i+1]`` (``first``: int32 [n+1]) of
     ``(frag_off, frag_len)``; each fragment is folded on its own like the reference,
     in one pass (``frag_sums`` is accepted for compatibility and unused).
+    ``runs``: RNS_FLAG_CHAIN_RUNS, the hint that fragments are often back-to-back
+    views of one buffer (same results either way).
     """
     _require_cuda(arena, "arena", (torch.uint8,))
     _require_cuda(frag_off, "frag_off", (torch.int64,))
@@ -285,7 +287,8 @@ def csum_chain(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch.Tens
     with torch.cuda.device(dev):
         st = lib.rns_csum_chain_dev(arena.data_ptr(), arena.numel(), frag_off.data_ptr(), frag_len.data_ptr(), nf,
                                     first.data_ptr(), seed_ptr, out.data_ptr(), n,
-                                    _lib.RNS_FLAG_COMPLEMENT if complement else 0, frag_len_hint,
+                                    (_lib.RNS_FLAG_COMPLEMENT if complement else 0) |
+                                    (_lib.RNS_FLAG_CHAIN_RUNS if runs else 0), frag_len_hint,
                                     frag_sums.data_ptr() if frag_sums is not None else None, bad_ptr,
                                     _stream_handle(dev))
     _lib.check(st, "rns_csum_chain_dev")

@@ -98,22 +98,28 @@ __device__ __forceinline__ uint32_t dpp_or_zero(uint32_t v)
         __builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, ROW_MASK, BANK_MASK, true));
 }
 
-// Exclusive prefix sum of the lanes' padded lengths: the classic gfx9 DPP scan
-// (row_shr 1,2,3 / 4 / 8 within each row of 16, then row_bcast:15 and row_bcast:31
-// across rows) — VALU only, no LDS round trip.
-__device__ __forceinline__ uint32_t packed_scan(const CsumArgs &a, uint32_t lane, uint32_t len)
+// Exclusive prefix sum over the 64 lanes (the total must fit 32 bits): the classic
+// gfx9 DPP scan (row_shr 1,2,3 / 4 / 8 within each row of 16, then row_bcast:15 and
+// row_bcast:31 across rows) — VALU only, no LDS round trip.  packed_scan applies it
+// to the lanes' padded lengths.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v)
 {
-    (void)lane;
-    const uint32_t pad = (len + a.align_mask) & ~a.align_mask;  // < 2^17: the block's sum fits 32 bits
-    uint32_t x = pad;
-    x += dpp_or_zero<0x111>(pad);            // row_shr:1
-    x += dpp_or_zero<0x112>(pad);            // row_shr:2
-    x += dpp_or_zero<0x113>(pad);            // row_shr:3
+    uint32_t x = v;
+    x += dpp_or_zero<0x111>(v);              // row_shr:1
+    x += dpp_or_zero<0x112>(v);              // row_shr:2
+    x += dpp_or_zero<0x113>(v);              // row_shr:3
     x += dpp_or_zero<0x114, 0xF, 0xE>(x);    // row_shr:4, banks 1-3
     x += dpp_or_zero<0x118, 0xF, 0xC>(x);    // row_shr:8, banks 2-3
     x += dpp_or_zero<0x142, 0xA, 0xF>(x);    // row_bcast:15 into rows 1 and 3
     x += dpp_or_zero<0x143, 0xC, 0xF>(x);    // row_bcast:31 into rows 2 and 3
-    return x - pad;
+    return x - v;
+}
+
+__device__ __forceinline__ uint32_t packed_scan(const CsumArgs &a, uint32_t lane, uint32_t len)
+{
+    (void)lane;
+    const uint32_t pad = (len + a.align_mask) & ~a.align_mask;  // < 2^17: the block's sum fits 32 bits
+    return wave_excl_scan(pad);
 }
 
 __device__ __forceinline__ uint64_t packed_off(const CsumArgs &a, uint64_t base, uint32_t lane, uint32_t len)
@@ -1031,12 +1037,15 @@ __device__ __forceinline__ uint32_t wave_class_pass(const CsumArgs &a, __amdgpu_
                                                     uint32_t d_len, uint32_t d_aux, uint32_t lane, uint4 *st,
                                                     uint32_t &pos, uint32_t d_seed = 0)
 {
-    // size class of this lane's packet; ranks within the class; sorted position
+    // size class of this lane's packet (kNumClasses: empty, no rounds at all — e.g. the
+    // fragments the chain kernel merged into their run's first); ranks within the
+    // class; sorted position (empty packets last)
     const uint32_t nch = d_len ? static_cast<uint32_t>(((d_start & 15) + d_len + 15) >> 4) : 0u;
     uint32_t cls = kNumClasses - 1;
 #pragma unroll
     for (int c = kNumClasses - 2; c >= 0; --c)
         cls = (nch <= kClassMax[c]) ? static_cast<uint32_t>(c) : cls;
+    cls = nch ? cls : kNumClasses;
     uint32_t rank = 0, off = 0;
     pos = 0;
     ClassRun cr[kNumClasses];
@@ -1051,6 +1060,12 @@ __device__ __forceinline__ uint32_t wave_class_pass(const CsumArgs &a, __amdgpu_
         }
         cr[c] = ClassRun{off, static_cast<uint32_t>(__popcll(m))};
         off += cr[c].cnt;
+    }
+    {
+        const uint64_t m = __ballot(cls == kNumClasses);
+        if (cls == kNumClasses)
+            pos = off + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
     }
     // next non-empty class after each class (wave-uniform); kNumClasses = none
     uint32_t next[kNumClasses + 1];
@@ -1570,20 +1585,84 @@ constexpr uint32_t kChainMaxK = 8;  // packets per lane, at most
 #endif
 constexpr bool kChainTiny = RNS_CHAIN_TINY && kTinyQ > 1;
 
+// Packets whose fragments form one run (RNS_FLAG_CHAIN_RUNS; A/B knob: -DRNS_CHAIN_RUNS=0).
+//
+// util.rs:112-119 folds after every fragment, each fragment's BE words paired from
+// its own start.  When fragment f starts where f-1 ends and f-1 has EVEN length, f's
+// words pair exactly as they do counted from f-1's start, so for fragments of at
+// most 128 KiB (no u32 wrap) fold(fold(s + W[f-1]) + W[f]) == fold(s + fold(W[f-1] +
+// W[f])): the same residue mod 0xffff, zero iff everything is zero.  A packet whose
+// fragments (at most kRunFrags) are such a run — the pieces of one receive buffer, as
+// the IP-trimmed views of a packet are — is therefore ONE contiguous unit of at most
+// 128 KiB.  When every packet of a wave batch is, the wave runs the class pass over
+// its 64 packets (as the plain batch kernel does) instead of over their fragments.
+// Opt-in: the check is a round of descriptor loads before the class pass, which a
+// layout without runs pays for nothing (profiles/r02_chain_runs_ab.json).
+#ifndef RNS_CHAIN_RUNS
+#define RNS_CHAIN_RUNS 1
+#endif
+constexpr bool kChainRuns = RNS_CHAIN_RUNS != 0;
+constexpr uint32_t kRunFrags = 4;
+constexpr uint32_t kNoRun = 0xFFFFFFFFu;
+
+// The bytes of packet [f0, f1)'s run, or kNoRun.  Its (<= kRunFrags) descriptors are
+// loaded up front: one memory latency, not one per fragment.
+__device__ __forceinline__ uint32_t fragment_run(const CsumArgs &a, uint32_t f0, uint32_t f1, uint64_t &start)
+{
+    const uint32_t nfr = f1 - f0;
+    if (nfr > kRunFrags)
+        return kNoRun;
+    uint64_t o[kRunFrags];
+    uint32_t l[kRunFrags];
+#pragma unroll
+    for (uint32_t j = 0; j < kRunFrags; ++j) {
+        o[j] = 0;
+        l[j] = 0;
+        if (j < nfr) {
+            o[j] = a.off[f0 + j] + a.base_adjust;
+            l[j] = a.len[f0 + j];
+        }
+    }
+    uint32_t tot = 0;
+    bool run = true;
+#pragma unroll
+    for (uint32_t j = 0; j < kRunFrags; ++j) {
+        if (j < nfr) {
+            const bool in = o[j] <= a.arena_bytes && l[j] <= a.arena_bytes - o[j];
+            const bool joins = j == 0 || (o[j] == o[j - 1] + l[j - 1] && !(l[j - 1] & 1));
+            run = run && in && joins && l[j] <= kNoWrapBytes;
+            tot += run ? l[j] : 0u;
+        }
+    }
+    start = o[0];
+    return run && tot <= kNoWrapBytes ? tot : kNoRun;
+}
+
 #ifndef RNS_CHAIN_OCC
 #define RNS_CHAIN_OCC 4
 #endif
-template <bool NT, bool BUF, uint32_t KMAX>
+// RUNS: the RNS_FLAG_CHAIN_RUNS instantiation (buffer path only).  A separate kernel:
+// compiled into the plain one, the run check cost it ~5 % (registers) even unused.
+template <bool NT, bool BUF, uint32_t KMAX, bool RUNS = false>
 __global__ __launch_bounds__(kBlock, RNS_CHAIN_OCC) void csum_chain_kernel(const CsumArgs a)
 {
+    static_assert(!RUNS || BUF, "runs: buffer path only");
     // A wave owns K*64 consecutive packets (K = a.chain_k, chosen by the host from the
     // mean fragment count so the wave's fragments fill whole 64-fragment batches).
     // Per-packet state is parked in LDS across the class pass (which needs every VGPR
     // of a 4-waves/SIMD budget): the fragment range and the running sum (bit 31 = a
     // bad descriptor seen).
-    __shared__ uint32_t pk_lds[kBlock / 64][3][KMAX * 64];
+    // RUNS: [3] the packet's run bytes (fragment_run), [4] its start
+    constexpr int kPk = RUNS ? 5 : 3;
+    __shared__ uint32_t pk_lds[kBlock / 64][kPk][KMAX * 64];
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t (&pk)[3][KMAX * 64] = pk_lds[threadIdx.x >> 6];
+    uint32_t (&pk)[kPk][KMAX * 64] = pk_lds[threadIdx.x >> 6];
+    // A wave stops looking for runs after a batch without them (the check costs a round
+    // of descriptor loads): the fragment path is exact for every batch anyway.
+#ifndef RNS_CHAIN_TRY  // A/B knob: 0 = the run code compiled in but never tried
+#define RNS_CHAIN_TRY 1
+#endif
+    bool try_runs = RUNS && RNS_CHAIN_TRY;
     const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
     const uint32_t K = KMAX == 1 ? 1u : a.chain_k;
@@ -1594,6 +1673,7 @@ __global__ __launch_bounds__(kBlock, RNS_CHAIN_OCC) void csum_chain_kernel(const
 
     for (uint64_t base = static_cast<uint64_t>(wave) * per_wave; base < a.n; base += nwaves * per_wave) {
         uint32_t lo_all = 0xFFFFFFFFu, hi_all = 0u;
+        bool runs_all = true;
         for (uint32_t q = 0; q < K; ++q) {
             const uint64_t p = base + q * 64 + lane;
             const bool live = p < a.n;
@@ -1607,16 +1687,31 @@ __global__ __launch_bounds__(kBlock, RNS_CHAIN_OCC) void csum_chain_kernel(const
             pk[0][q * 64 + lane] = f0;
             pk[1][q * 64 + lane] = f1;
             pk[2][q * 64 + lane] = acc | (ok ? 0u : kBad);
+            if constexpr (RUNS) {
+                uint64_t rs = 0;
+                const uint32_t run = (ok && try_runs) ? fragment_run(a, f0, f1, rs) : kNoRun;
+                pk[RUNS ? 3 : 0][q * 64 + lane] = run;
+                pk[RUNS ? 4 : 0][q * 64 + lane] = static_cast<uint32_t>(rs);  // < 4 GiB on the buffer path
+                runs_all = runs_all && run != kNoRun;
+            }
         }
         // the wave's fragments: the union of its packets' ranges (contiguous for a CSR list)
         const uint32_t F0 = wave_min_u32(lo_all), F1 = wave_max_u32(hi_all);
-        for (uint64_t fb = F0; fb < F1; fb += 64) {
-            const uint64_t f = fb + lane;
+        // every packet one run: K class passes over packets; else passes over fragments
+        const bool by_packet = RUNS && try_runs && !__ballot(!runs_all);
+        try_runs = by_packet;
+        const uint32_t passes = by_packet ? K : (F1 - F0 + 63) / 64;  // (F1 >= F0, equal if no fragments)
+        for (uint32_t it = 0; it < passes; ++it) {
+            const uint64_t fb = F0 + 64ull * it;
             uint64_t d_start = 0;
             uint32_t d_len = 0;
-            if (f < F1) {
-                d_start = a.off[f];
-                d_len = a.len[f];
+            if (by_packet) {
+                const uint32_t i = it * 64 + lane;
+                d_len = pk[RUNS ? 3 : 0][i];
+                d_start = pk[RUNS ? 4 : 0][i] - a.base_adjust;  // (base_adjust added back below)
+            } else if (fb + lane < F1) {
+                d_start = a.off[fb + lane];
+                d_len = a.len[fb + lane];
             }
             d_start += a.base_adjust;
             const bool d_ok = d_start <= a.arena_bytes && d_len <= a.arena_bytes - d_start;
@@ -1635,6 +1730,12 @@ __global__ __launch_bounds__(kBlock, RNS_CHAIN_OCC) void csum_chain_kernel(const
             }
             const uint32_t gflag = (big ? 1u : 0u) | (d_ok ? 0u : 2u);
             wave_lds_fence();
+            if (by_packet) {  // the lane's packet is its run: one fold (never big, never bad)
+                const uint32_t i = it * 64 + lane;
+                const uint32_t s = (pk[2][i] & 0xffffu) + g;
+                pk[2][i] = (s & 0xffff) + (s >> 16);
+                continue;
+            }
             // owner lanes: each packet's fragments inside [fb, fb + 64), in order
             for (uint32_t q = 0; q < K; ++q) {
                 const uint32_t i = q * 64 + lane;
@@ -2114,8 +2215,14 @@ int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
     const bool nt = (frag_len_hint ? frag_len_hint : 512u) >= 384u;
 #endif
     const bool buf = buf_records(a) < kOobOffset;
+    // RNS_FLAG_CHAIN_RUNS: the run-checking kernel (buffer path; a hint, ignored otherwise)
+    const bool runs = kChainRuns && (flags & RNS_FLAG_CHAIN_RUNS) && buf;
 #define RNS_CHAIN_LAUNCH(KM)                                                                      \
-    if (nt && buf)                                                                                \
+    if (runs && nt)                                                                               \
+        hipLaunchKernelGGL((csum_chain_kernel<true, true, KM, true>), grid, block, 0, st, a);     \
+    else if (runs)                                                                                \
+        hipLaunchKernelGGL((csum_chain_kernel<false, true, KM, true>), grid, block, 0, st, a);    \
+    else if (nt && buf)                                                                           \
         hipLaunchKernelGGL((csum_chain_kernel<true, true, KM>), grid, block, 0, st, a);           \
     else if (nt)                                                                                  \
         hipLaunchKernelGGL((csum_chain_kernel<true, false, KM>), grid, block, 0, st, a);          \

@@ -22,12 +22,12 @@ def host_u16(t):
     return t.view(torch.int16).cpu().numpy().view(np.uint16)
 
 
-def run_chain(arena_t, offs, lens, first, seeds, complement=False, bad=None):
+def run_chain(arena_t, offs, lens, first, seeds, complement=False, bad=None, runs=False):
     return host_u16(csum_chain(arena_t, dev(np.asarray(offs, dtype=np.uint64), np.int64),
                                dev(np.asarray(lens, dtype=np.uint32), np.int32),
                                dev(np.asarray(first, dtype=np.uint32), np.int32),
                                None if seeds is None else dev(np.asarray(seeds, dtype=np.uint16), np.int16),
-                               complement=complement, bad=bad))
+                               complement=complement, bad=bad, runs=runs))
 
 
 def test_reference_kats():
@@ -81,6 +81,7 @@ def test_full_size_received_fragments_match_contiguous(oracle):
     first = np.arange(0, 3 * lay.n + 1, 3, dtype=np.uint32)
     got = run_chain(b.arena, offs, lens, first, lay.seed, complement=True)
     assert np.array_equal(got, contiguous)
+    assert np.array_equal(run_chain(b.arena, offs, lens, first, lay.seed, complement=True, runs=True), contiguous)
     sample = slice(0, 20000)
     arena_np = b.arena[:int(lay.off[20000])].cpu().numpy()
     expect = oracle.chain_batch(arena_np, offs[:60000], lens[:60000], first[:20001], lay.seed[sample], complement=True)
@@ -120,8 +121,10 @@ def test_many_fragments_no_overflow(oracle):
     seeds = np.array([0xfffe, 1, 0, 0xffff], dtype=np.uint16)
     for complement in (False, True):
         expect = oracle.chain_batch(arena_np, offs, lens, first, seeds, complement=complement)
-        got = run_chain(torch.from_numpy(arena_np).to(DEV), offs, lens, first, seeds, complement=complement)
-        assert np.array_equal(got, expect)
+        for runs in (False, True):
+            got = run_chain(torch.from_numpy(arena_np).to(DEV), offs, lens, first, seeds, complement=complement,
+                            runs=runs)
+            assert np.array_equal(got, expect)
 
 
 @pytest.mark.parametrize("fill", [0xff, None])
@@ -190,3 +193,145 @@ def test_packets_without_fragments():
     assert np.array_equal(got, np.arange(100, dtype=np.uint16))
     got = run_chain(a, [], [], [0] * 101, list(range(100)), complement=True)
     assert np.array_equal(got, (0xffff ^ np.arange(100)).astype(np.uint16))
+
+
+def _adjacent_chains(n, seed, arena_size, max_len, p_odd, p_jump):
+    """Chains laid out as runs of adjacent fragments (each fragment starts where the
+    previous one ends, across packet boundaries too), with odd lengths, empty
+    fragments, long fragments and occasional jumps to a fresh offset."""
+    w = O.splitmix64_words(seed, n)
+    nfr = (w % np.uint64(9)).astype(np.int64)
+    first = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(nfr, out=first[1:])
+    nf = int(first[-1])
+    fw = O.splitmix64_words(seed + 1, nf)
+    lens = ((fw % np.uint64(max_len)) & ~np.uint64(1)).astype(np.int64)       # even ...
+    odd = (fw >> np.uint64(32)) % np.uint64(1000) < np.uint64(int(p_odd * 1000))
+    lens[odd] += 1                                                              # ... or odd
+    lens[(fw >> np.uint64(44)) % np.uint64(50) == 0] = 0                        # empty fragments
+    jump = (fw >> np.uint64(52)) % np.uint64(1000) < np.uint64(int(p_jump * 1000))
+    offs = np.zeros(nf, dtype=np.int64)
+    pos = 0
+    for i in range(nf):   # (a few 10K fragments: a Python loop is fine)
+        if jump[i]:
+            pos = int(fw[i] >> np.uint64(20)) % (arena_size // 2)
+        if pos + lens[i] > arena_size:
+            pos = 0
+        offs[i] = pos
+        pos += int(lens[i])
+    seeds = (w >> np.uint64(40) & np.uint64(0xFFFF)).astype(np.uint16)
+    return offs.astype(np.uint64), lens.astype(np.uint32), first.astype(np.uint32), seeds
+
+
+@pytest.mark.parametrize("max_len,p_odd", [(1600, 0.1), (600, 0.4), (70_000, 0.05), (300_000, 0.1)])
+def test_adjacent_fragment_runs(oracle, max_len, p_odd):
+    """Runs of adjacent fragments, with and without RNS_FLAG_CHAIN_RUNS: runs that cross
+    packet boundaries, odd lengths mid-run, empty fragments, runs longer than 128 KiB
+    and fragments past 128 KiB must all fold exactly as the reference's per-fragment
+    loop (util.rs:112-119)."""
+    n = 20_000 if max_len <= 1600 else 2_000
+    size = 16 << 20
+    arena_np = O.splitmix64_bytes(0xAD1 + max_len, size)
+    offs, lens, first, seeds = _adjacent_chains(n, 0xAD2 + max_len, size, max_len, p_odd, 0.05)
+    expect = oracle.chain_batch(arena_np, offs, lens, first, seeds, complement=True)
+    for runs in (False, True):
+        got = run_chain(torch.from_numpy(arena_np).to(DEV), offs, lens, first, seeds, complement=True, runs=runs)
+        assert np.array_equal(got, expect)
+
+
+def test_adjacent_runs_all_ones_wrap_edges(oracle):
+    """0xff runs whose merged sum sits at the fold edges: 65 536 bytes of 0xff in 64
+    adjacent 1 KiB fragments (sum == 0 mod 0xffff, non-zero), a run of exactly 128 KiB,
+    one byte past it, and zero runs after a zero seed."""
+    arena_np = np.full(3 << 20, 0xff, dtype=np.uint8)
+    arena_np[2 << 20:] = 0
+    offs, lens, first = [], [], [0]
+    pos = 0
+    for frag_len, count in ((1024, 64), (2048, 64), (2048, 64), (4096, 33)):
+        for _ in range(count):
+            offs.append(pos)
+            lens.append(frag_len)
+            pos += frag_len
+        first.append(len(offs))
+    lens[-1] = 4095                 # last run: 32*4096 + 4095 bytes (past 128 KiB), odd tail
+    for _ in range(64):             # zero bytes, zero seed
+        offs.append((2 << 20) + 512 * (len(offs) % 64))
+        lens.append(512)
+    first.append(len(offs))
+    offs, lens = np.array(offs, dtype=np.uint64), np.array(lens, dtype=np.uint32)
+    first = np.array(first, dtype=np.uint32)
+    for seeds in (np.array([0, 1, 0xffff, 0xfffe, 0], dtype=np.uint16), None):
+        for complement in (False, True):
+            expect = oracle.chain_batch(arena_np, offs, lens, first, seeds, complement=complement)
+            for runs in (False, True):
+                got = run_chain(torch.from_numpy(arena_np).to(DEV), offs, lens, first, seeds, complement=complement,
+                                runs=runs)
+                assert np.array_equal(got, expect)
+
+
+def test_adjacent_runs_overlapping_ranges(oracle):
+    """Malformed CSR whose VALID ranges overlap: a run of adjacent fragments must never
+    carry one packet's fragments into another's sum."""
+    arena_np = O.splitmix64_bytes(0xAD9, 1 << 20)
+    nf = 40
+    lens = np.full(nf, 100, dtype=np.uint32)
+    offs = np.arange(nf, dtype=np.uint64) * np.uint64(100)          # one long adjacent run
+    first = np.array([0, 6, 4, 8, 13, 12, 20, 40], dtype=np.uint32)  # [0,6) [6,4)x [4,8) [8,13) [13,12)x [12,20) [20,40)
+    seeds = np.arange(7, dtype=np.uint16) * np.uint16(1000)
+    lo, hi = first[:-1].astype(np.int64), first[1:].astype(np.int64)
+    valid = (lo <= hi) & (hi <= nf)
+    idx = [np.arange(a, b) for a, b in zip(lo[valid], hi[valid])]
+    sub_first = np.zeros(int(valid.sum()) + 1, dtype=np.uint32)
+    np.cumsum([len(i) for i in idx], out=sub_first[1:])
+    cat = np.concatenate(idx)
+    expect = oracle.chain_batch(arena_np, offs[cat], lens[cat], sub_first, seeds[valid], complement=True)
+    for runs in (False, True):
+        got = run_chain(torch.from_numpy(arena_np).to(DEV), offs, lens, first, seeds, complement=True, runs=runs)
+        assert np.array_equal(got[valid], expect)
+        assert (got[~valid] == 0).all()
+
+
+@pytest.mark.parametrize("break_every,max_len", [(0, 3000), (997, 3000), (0, 40_000), (0, 64)])
+def test_runs_by_packet(oracle, break_every, max_len):
+    """Every packet's fragments one run (0-4 adjacent fragments, all but the last of even
+    length, at any start parity, empty fragments included): the wave sums each packet as
+    one contiguous unit.  break_every: every n-th packet gets a gap or an odd middle
+    fragment, so its wave takes the per-fragment path while the others do not."""
+    n = 30_000 if max_len <= 3000 else 3_000
+    size = 64 << 20
+    arena_np = O.splitmix64_bytes(0xB00 + max_len, size)
+    w = O.splitmix64_words(0xB01 + break_every, n)
+    nfr = (w % np.uint64(5)).astype(np.int64)
+    first = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(nfr, out=first[1:])
+    nf = int(first[-1])
+    fw = O.splitmix64_words(0xB02, nf)
+    lens = (fw % np.uint64(max_len + 1)).astype(np.int64)
+    last = np.zeros(nf, dtype=bool)
+    last[first[1:][nfr > 0] - 1] = True
+    lens[~last] &= ~1                                      # even, except each packet's last fragment
+    lens[(fw >> np.uint64(40)) % np.uint64(40) == 0] = 0   # empty fragments
+    start = ((w >> np.uint64(16)) % np.uint64(size - 5 * max_len - 16)).astype(np.int64)
+    offs = np.zeros(nf, dtype=np.int64)
+    for p in range(n):
+        pos = int(start[p])
+        for f in range(int(first[p]), int(first[p + 1])):
+            offs[f] = pos
+            pos += int(lens[f])
+    if break_every:
+        for p in range(0, n, break_every):
+            f0, f1 = int(first[p]), int(first[p + 1])
+            if f1 - f0 >= 2:
+                if p % 2:
+                    offs[f0 + 1:f1] += 2           # a gap
+                else:
+                    lens[f0] |= 1                  # an odd fragment before the last
+                    offs[f0 + 1:f1] += 1
+    seeds = (w >> np.uint64(40) & np.uint64(0xFFFF)).astype(np.uint16)
+    offs, lens, first = offs.astype(np.uint64), lens.astype(np.uint32), first.astype(np.uint32)
+    for complement in (False, True):
+        expect = oracle.chain_batch(arena_np, offs, lens, first, seeds, complement=complement)
+        for runs in (False, True):
+            got = run_chain(torch.from_numpy(arena_np).to(DEV), offs, lens, first, seeds, complement=complement,
+                            runs=runs)
+            assert np.array_equal(got, expect)

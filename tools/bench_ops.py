@@ -79,9 +79,11 @@ def main():
     ap.add_argument("--configs", default="c3_1500B,c5_imix")
     ap.add_argument("--ops", default="csum,chain,fill,verify,tx")
     ap.add_argument("--out", default="")
-    ap.add_argument("--chain-layouts", default="packed,netbuf",
+    ap.add_argument("--chain-layouts", default="packed,netbuf,netbuf_shuffled",
                     help="packed: [492, 512, rest] fragments back to back inside each packet; netbuf: every "
-                         "fragment in its own 512-byte buffer (NetBuffer, buf.rs:50), ceil(L/512) per packet")
+                         "fragment in its own 512-byte buffer (NetBuffer, buf.rs:50), ceil(L/512) per packet, "
+                         "the buffers in order (a packet's fragments adjacent); netbuf_shuffled: the same "
+                         "buffers in a random order (no two fragments adjacent)")
     args = ap.parse_args()
     ops = set(args.ops.split(","))
     dev = torch.device("cuda:0")
@@ -99,7 +101,9 @@ def main():
         if "chain" in ops:
             for cl in args.chain_layouts.split(","):
                 key = "chain" if cl == "packed" else f"chain_{cl}"
-                r[key] = bench_chain(b, lay, dev, args) if cl == "packed" else bench_chain_netbuf(lay, dev, args)
+                for runs in (False, True):  # without / with RNS_FLAG_CHAIN_RUNS
+                    r[key + ("_runs" if runs else "")] = bench_chain(b, lay, dev, args, runs) if cl == "packed" else \
+                        bench_chain_netbuf(lay, dev, args, shuffled=cl == "netbuf_shuffled", runs=runs)
         if "fill" in ops:
             ms = timed(lambda: csum_fill(b.arena, b.off, b.length, b.seed, field_off=16), args.steps, args.rounds)
             r["fill"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1)}
@@ -131,7 +135,7 @@ def main():
     print(json.dumps(results))
 
 
-def bench_chain(b, lay, dev, args):
+def bench_chain(b, lay, dev, args, runs=False):
     n, pay = lay.n, lay.payload_bytes
     # chain: three fragments per packet where the packet is long enough, else one
     L = lay.length.astype(np.int64)
@@ -158,15 +162,16 @@ def bench_chain(b, lay, dev, args):
     sums = torch.empty(nf, dtype=torch.uint16, device=dev)
     out = torch.empty(n, dtype=torch.uint16, device=dev)
     ms = timed(lambda: csum_chain(b.arena, d_fo, d_fl, d_first, b.seed, complement=True, out=out,
-                                  frag_sums=sums, frag_len_hint=int(round(pay / nf))),
+                                  frag_sums=sums, frag_len_hint=int(round(pay / nf)), runs=runs),
                args.steps, args.rounds)
     return {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1), "fragments": nf}
 
 
-def bench_chain_netbuf(lay, dev, args):
+def bench_chain_netbuf(lay, dev, args, shuffled=False, runs=False):
     """Fragments as NetBuffer holds them: packet i of L bytes is ceil(L/512) fragments,
     each in its own 512-byte buffer (buf.rs:50; the fragment arena is those buffers
-    back to back, filled with splitmix64 bytes)."""
+    back to back, filled with splitmix64 bytes).  shuffled: fragment f lives in buffer
+    perm[f] (a random permutation), as buffers from a free list are."""
     from rustnetworkstack_amd.batch import fill_splitmix64
     n, pay = lay.n, lay.payload_bytes
     L = lay.length.astype(np.int64)
@@ -176,7 +181,8 @@ def bench_chain_netbuf(lay, dev, args):
     nf = int(first[-1])
     pkt = np.repeat(np.arange(n), nfr)
     k = np.arange(nf) - first[:-1][pkt]
-    frag_off = (np.arange(nf, dtype=np.uint64) * np.uint64(512))
+    slot = np.random.default_rng(0x5B0F).permutation(nf) if shuffled else np.arange(nf)
+    frag_off = slot.astype(np.uint64) * np.uint64(512)
     frag_len = np.minimum(L[pkt] - 512 * k, 512).astype(np.uint32)
     arena = torch.empty(nf * 512 + 16, dtype=torch.uint8, device=dev)
     fill_splitmix64(arena, 0xF4A6)
@@ -186,12 +192,12 @@ def bench_chain_netbuf(lay, dev, args):
     seed = torch.from_numpy(lay.seed.view(np.int16)).to(dev)
     out = torch.empty(n, dtype=torch.uint16, device=dev)
     ms = timed(lambda: csum_chain(arena, d_fo, d_fl, d_first, seed, complement=True, out=out,
-                                  frag_len_hint=int(round(pay / nf))),
+                                  frag_len_hint=int(round(pay / nf)), runs=runs),
                args.steps, args.rounds)
     del arena
     torch.cuda.empty_cache()
     return {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1), "fragments": nf,
-            "layout": "netbuf: 512-byte fragment buffers"}
+            "layout": "netbuf: 512-byte fragment buffers" + (", shuffled" if shuffled else ", in order")}
 
 
 if __name__ == "__main__":
