@@ -2645,7 +2645,7 @@ const char *rns_csum_shape_name(uint32_t len_hint)
     static thread_local char buf[96];
     const Shape sh = pick_shape(len_hint);
     if (sh.variant & 4)
-        std::snprintf(buf, sizeof(buf), "%s (size classes G/U 4/1, 4/4, 16/4, 32/4, 64/4)", names[sh.variant & 7]);
+        std::snprintf(buf, sizeof(buf), "%s (size classes G/U 4/1 x 4 packets, 4/4, 16/4, 32/4, 64/4)", names[sh.variant & 7]);
     else
         std::snprintf(buf, sizeof(buf), "%s<G=%u,U=%u>%s%s", names[sh.variant & 7], sh.G, sh.U,
                       (sh.variant & 8) ? " all rounds in flight" : (sh.variant & 16) ? " descriptors prefetched" : "",

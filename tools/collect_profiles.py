@@ -3,8 +3,9 @@
     python tools/collect_profiles.py r01i --round r01
 
 Writes profiles/<round>_bench_<config>.json (the bench JSON lines),
-profiles/<round>_rocprof_kernel_stats.csv / _kernel_trace.csv (rocprofv3
---kernel-trace --stats of `bench.py`), profiles/traffic_<config>.json (PMC
+profiles/<round>_rocprof_bench_<config>.json / _timed_stats.csv / _kernel_stats.csv
+(tools/gpu_session.sh: rocprofv3 --kernel-trace --stats of that same bench command,
+reconciled by tools/profile_bench.py), profiles/traffic_<config>.json (PMC
 FETCH_SIZE/WRITE_SIZE per launch, read by bench.py) and the sweep JSON if present.
 """
 import argparse
@@ -32,11 +33,6 @@ def main():
                 cfg = d["config"]["workload"].split(":")[0]
                 with open(os.path.join(dst, f"{args.round}_bench_{cfg}.json"), "w") as f:
                     json.dump(d, f, indent=1)
-    prof = os.path.join(src, "prof")
-    for kind in ("kernel_stats", "kernel_trace"):
-        p = os.path.join(prof, f"run_{kind}.csv")
-        if os.path.exists(p):
-            shutil.copy(p, os.path.join(dst, f"{args.round}_rocprof_c3_1500B_{kind}.csv"))
     for name in os.listdir(src):
         if name.startswith("traffic_") and name.endswith(".json"):
             d = json.load(open(os.path.join(src, name)))
@@ -45,6 +41,19 @@ def main():
             d["collected"] = f"{args.round} gpurun session {args.tag}"
             with open(os.path.join(dst, name), "w") as f:
                 json.dump(d, f, indent=1)
+    # tools/gpu_session.sh: the bench line and the rocprofv3 trace of that same command
+    for name in os.listdir(src):
+        if name.startswith("rocprof_bench_") and name.endswith(".json"):
+            cfg = name[len("rocprof_bench_"):-len(".json")]
+            d = json.load(open(os.path.join(src, name)))
+            d["collected"] = f"{args.round} gpurun session {args.tag}"
+            with open(os.path.join(dst, f"{args.round}_rocprof_bench_{cfg}.json"), "w") as f:
+                json.dump(d, f, indent=1)
+            for suffix, srcname in (("_timed_stats.csv", f"rocprof_bench_{cfg}_timed_stats.csv"),
+                                    ("_kernel_stats.csv", os.path.join("prof", "run_kernel_stats.csv"))):
+                sp = os.path.join(src, srcname)
+                if os.path.exists(sp):
+                    shutil.copy(sp, os.path.join(dst, f"{args.round}_rocprof_bench_{cfg}{suffix}"))
     sw = os.path.join(src, "sweep.log")
     if os.path.exists(sw):
         lines = [ln for ln in open(sw) if ln.startswith("{")]
