@@ -1963,8 +1963,12 @@ int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
                                a);
     } else if ((sh.variant & ~16u) == 3u && sh.G == 4u && sh.U == 1u) {  // c2: 13.46 -> 13.36 us with prefetch
         const bool pf = (sh.variant & 16u) != 0;
+#ifndef RNS_PACKED_TINY_D  // A/B knob: 4 = every round of a wave batch issued at once (with the prefetch)
+#define RNS_PACKED_TINY_D 1
+#endif
         if (buf && pf)
-            hipLaunchKernelGGL((csum_rounds_kernel<4, 1, false, true, true, 1, true, true>), grid, block, 0, st, a);
+            hipLaunchKernelGGL((csum_rounds_kernel<4, 1, false, true, true, RNS_PACKED_TINY_D, true, true>), grid, block, 0,
+                               st, a);
         else if (buf)
             hipLaunchKernelGGL((csum_rounds_kernel<4, 1, false, true, true, 1, true>), grid, block, 0, st, a);
         else if (pf)
