@@ -1302,12 +1302,17 @@ __device__ __forceinline__ Desc<BUF> load_desc(const CsumArgs &a, uint64_t p)
     return d;
 }
 
-// Workgroup size of the mixed kernel: receive verify and transmit fill hold an LDS
-// stash per wave, and LDS is freed per WORKGROUP, so one-wave workgroups let a CU
-// refill as soon as any wave finishes (IMIX verify 590 -> 559 us); the plain batch
-// has no LDS and keeps 4-wave workgroups.
+// Workgroup size of the mixed kernel: one wave.  Receive verify and transmit fill hold
+// an LDS stash per wave, and LDS is freed per WORKGROUP, so one-wave workgroups let a
+// CU refill as soon as any wave finishes (IMIX verify 590 -> 559 us).  The plain batch
+// has no LDS, but a new workgroup still waits for a slot for ALL its waves: one-wave
+// workgroups took IMIX from 440-456 to 424-430 us per pipelined step (c3 equal;
+// profiles/r02_block_ab.json).  A/B knob: -DRNS_MIXED_PLAIN_BLOCK=256.
+#ifndef RNS_MIXED_PLAIN_BLOCK
+#define RNS_MIXED_PLAIN_BLOCK 64
+#endif
 template <bool STASH>
-constexpr int kMixedBlock = STASH ? 64 : kBlock;
+constexpr int kMixedBlock = STASH ? 64 : RNS_MIXED_PLAIN_BLOCK;
 
 // FILL (transmit in-place fill, tcp.rs:957-973 / udp.rs:158-171 / icmp.rs:87-112 /
 // ip.rs:158-159): the checksum is that of the packet with its 2-byte field zeroed
@@ -1641,10 +1646,17 @@ __device__ __forceinline__ uint32_t fragment_run(const CsumArgs &a, uint32_t f0,
 #ifndef RNS_CHAIN_OCC
 #define RNS_CHAIN_OCC 4
 #endif
+// Workgroup size of the chain kernel: one wave.  Its per-packet state is LDS, which is
+// freed per workgroup, as for the mixed kernel's stash modes: IMIX chains 640 -> 608 us
+// packed, 839 -> 771 us in 512-byte buffers, c3 equal (profiles/r02_block_ab.json).
+#ifndef RNS_CHAIN_BLOCK
+#define RNS_CHAIN_BLOCK 64
+#endif
+constexpr int kChainBlock = RNS_CHAIN_BLOCK;
 // RUNS: the RNS_FLAG_CHAIN_RUNS instantiation (buffer path only).  A separate kernel:
 // compiled into the plain one, the run check cost it ~5 % (registers) even unused.
 template <bool NT, bool BUF, uint32_t KMAX, bool RUNS = false>
-__global__ __launch_bounds__(kBlock, RNS_CHAIN_OCC) void csum_chain_kernel(const CsumArgs a)
+__global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(const CsumArgs a)
 {
     static_assert(!RUNS || BUF, "runs: buffer path only");
     // A wave owns K*64 consecutive packets (K = a.chain_k, chosen by the host from the
@@ -1654,7 +1666,7 @@ __global__ __launch_bounds__(kBlock, RNS_CHAIN_OCC) void csum_chain_kernel(const
     // bad descriptor seen).
     // RUNS: [3] the packet's run bytes (fragment_run), [4] its start
     constexpr int kPk = RUNS ? 5 : 3;
-    __shared__ uint32_t pk_lds[kBlock / 64][kPk][KMAX * 64];
+    __shared__ uint32_t pk_lds[kChainBlock / 64][kPk][KMAX * 64];
     const uint32_t lane = threadIdx.x & 63;
     uint32_t (&pk)[kPk][KMAX * 64] = pk_lds[threadIdx.x >> 6];
     // A wave stops looking for runs after a batch without them (the check costs a round
@@ -1663,8 +1675,8 @@ __global__ __launch_bounds__(kBlock, RNS_CHAIN_OCC) void csum_chain_kernel(const
 #define RNS_CHAIN_TRY 1
 #endif
     bool try_runs = RUNS && RNS_CHAIN_TRY;
-    const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
+    const uint32_t wave = (blockIdx.x * kChainBlock + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * kChainBlock) >> 6;
     const uint32_t K = KMAX == 1 ? 1u : a.chain_k;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
@@ -1817,13 +1829,14 @@ int launch_shape(const CsumArgs &a, uint32_t variant, uint32_t max_blocks, hipSt
         blocks = (static_cast<uint64_t>(a.n) + kGroups - 1) / kGroups;
     } else {
         const uint64_t batches = (static_cast<uint64_t>(a.n) + 63) / 64;  // one wave per 64 packets
-        blocks = (batches + kBlock / 64 - 1) / (kBlock / 64);
+        const uint64_t wpb = ((variant & 4) ? kMixedBlock<false> : kBlock) / 64;  // waves per workgroup
+        blocks = (batches + wpb - 1) / wpb;
     }
     if (max_blocks != 0 && blocks > max_blocks)
         blocks = max_blocks;
     if (blocks == 0)
         return RNS_OK;
-    const dim3 grid(static_cast<uint32_t>(blocks)), block(kBlock);
+    const dim3 grid(static_cast<uint32_t>(blocks)), block((variant & 4) ? kMixedBlock<false> : kBlock);
     const bool nt = (variant & 2) != 0;
     const bool buf = buf_records(a) < kOobOffset;  // buffer loads need a 32-bit offset range
     // Variant bits 8-11 (tuning): at most that many workgroups per CU, i.e. waves per
@@ -1928,15 +1941,18 @@ struct Shape {
     uint32_t variant, G, U, max_blocks;
 };
 
+#ifndef RNS_MIXED_GRID_CAP  // A/B knob: at most this many workgroups for the mixed kernel (0 = one wave per batch)
+#define RNS_MIXED_GRID_CAP 0
+#endif
 Shape pick_shape(uint32_t len_hint)
 {
     const uint32_t chunks = len_hint ? (len_hint + 15) / 16 + 1 : 96;
     if (chunks <= 8)  // rounds, nontemporal, next batch's descriptors prefetched (c2: 15.1 -> 14.4 us)
         return Shape{19u, 4u, 1u, 2048u};
     if (chunks <= 48)
-        return Shape{4u, 0u, 0u, 0u};
+        return Shape{4u, 0u, 0u, RNS_MIXED_GRID_CAP};
     if (chunks <= 160)
-        return Shape{6u, 0u, 0u, 0u};
+        return Shape{6u, 0u, 0u, RNS_MIXED_GRID_CAP};
     return Shape{2u, 64u, 4u, 0u};
 }
 
@@ -1947,10 +1963,11 @@ int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
 {
     const bool nt = (sh.variant & 2u) != 0, buf = buf_records(a) < kOobOffset;
     const uint64_t batches = (static_cast<uint64_t>(a.n) + 63) / 64;  // one wave per 64 packets
-    uint64_t blocks = (batches + kBlock / 64 - 1) / (kBlock / 64);
+    const uint64_t wpb = ((sh.variant & 4u) ? kMixedBlock<false> : kBlock) / 64;  // waves per workgroup
+    uint64_t blocks = (batches + wpb - 1) / wpb;
     if (sh.max_blocks != 0 && blocks > sh.max_blocks)
         blocks = sh.max_blocks;
-    const dim3 grid(static_cast<uint32_t>(blocks)), block(kBlock);
+    const dim3 grid(static_cast<uint32_t>(blocks)), block((sh.variant & 4u) ? kMixedBlock<false> : kBlock);
     if (sh.variant & 4u) {
         if (nt && buf)
             hipLaunchKernelGGL((csum_mixed_kernel<false, true, true, false, false, false, true>), grid, block, 0, st, a);
@@ -2206,7 +2223,7 @@ int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
     }
     a.chain_k = K;
     const uint64_t waves = (static_cast<uint64_t>(n_pkts) + 64 * K - 1) / (64 * K);
-    const dim3 grid(static_cast<uint32_t>((waves + kBlock / 64 - 1) / (kBlock / 64))), block(kBlock);
+    const dim3 grid(static_cast<uint32_t>((waves + kChainBlock / 64 - 1) / (kChainBlock / 64))), block(kChainBlock);
     hipStream_t st = static_cast<hipStream_t>(stream);
     // nontemporal loads for long fragments, as pick_shape chooses for packets
     // Nontemporal loads for NetBuffer-sized fragments (c3 as 3 fragments: 298 -> 289 us
