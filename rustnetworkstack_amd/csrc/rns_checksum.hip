@@ -1313,6 +1313,11 @@ __device__ __forceinline__ Desc<BUF> load_desc(const CsumArgs &a, uint64_t p)
 #endif
 template <bool STASH>
 constexpr int kMixedBlock = STASH ? 64 : RNS_MIXED_PLAIN_BLOCK;
+// A/B knob: packed descriptors of the next wave batch loaded beside this batch's seeds.
+#ifndef RNS_MIXED_PACKED_PF
+#define RNS_MIXED_PACKED_PF 1
+#endif
+constexpr bool kMixedPackedPf = RNS_MIXED_PACKED_PF != 0;
 
 // FILL (transmit in-place fill, tcp.rs:957-973 / udp.rs:158-171 / icmp.rs:87-112 /
 // ip.rs:158-159): the checksum is that of the packet with its 2-byte field zeroed
@@ -1345,10 +1350,33 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX
     // live registers spill at 4 waves/SIMD and the spill forces a wait on the loads.)
     const uint64_t wstep = static_cast<uint64_t>(nwaves) * kPer;
 
+    // Packed form: the next wave batch's lengths (and block base) are loaded together
+    // with this batch's seeds after the class pass — one memory latency between two
+    // batches instead of two, and nothing extra is live during the class pass.
+    constexpr bool kPf = PACKED && kMixedPackedPf;
+    uint32_t nx_len = 0;
+    uint64_t nx_blk = 0;
+    auto load_next = [&](uint64_t b) {  // branch-free: past the end re-reads the last packet
+        const uint64_t q = b + lane < a.n ? b + lane : a.n - 1;
+        nx_len = a.len16[q];
+        nx_blk = a.blk_off[(b < a.n ? b : a.n - 1) >> 6];
+    };
+    if constexpr (kPf)
+        load_next(static_cast<uint64_t>(wave) * kPer);
+
     for (uint64_t base = static_cast<uint64_t>(wave) * kPer; base < a.n; base += wstep) {
         const uint64_t p = base + lane;
         const bool live = p < a.n;
-        const Desc<BUF> cd = load_desc<STRIDED, FILL, BUF, PACKED>(a, p);
+        Desc<BUF> cd;
+        if constexpr (kPf) {
+            cd.len = live ? nx_len : 0u;
+            const uint64_t off = nx_blk + packed_scan(a, lane, cd.len);
+            cd.off = BUF ? (off > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(off)) : off;
+            cd.off = live ? cd.off : 0;
+            cd.field = 0xFFFFFFFFu;
+        } else {
+            cd = load_desc<STRIDED, FILL, BUF, PACKED>(a, p);
+        }
         uint64_t d_start = cd.off + a.base_adjust;
         // the seed is first needed after the data pass: loaded here, its latency is hidden
         uint32_t d_len = cd.len;
@@ -1528,8 +1556,13 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX
             fs = fill_site(a, d_start, d_len, d_field, big, reinterpret_cast<const uint8_t *>(st + pos * kNS), d_ok);
             mine -= fs.contrib;
         }
-        if constexpr (PACKED)
+        if constexpr (PACKED) {
+#ifndef RNS_DIAG_NOSEED  // diagnostic A/B only (wrong results): what the seed load's latency costs
             d_seed = (a.seed && live) ? a.seed[p] : 0u;
+#endif
+            if constexpr (kPf)
+                load_next(base + wstep);  // in flight while this batch finishes and stores
+        }
         uint16_t res;
         if constexpr (FILL && kFillInRound)
             res = d_ok ? static_cast<uint16_t>(mine) : static_cast<uint16_t>(0);  // finished (and stored) in-round
