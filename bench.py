@@ -45,6 +45,8 @@ if ROOT not in sys.path:
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip-level table)
 METRIC = "GiB/s device-resident Internet checksum, 1500B-packet batches, 1/2/4/8 GPUs"
+# --op verify (not the headline): receive verify of IPv4/TCP datagrams (rns_rx_verify_dev)
+METRIC_VERIFY = "GiB/s device-resident receive verify (ip.rs:76 + tcp.rs:838-850), IPv4/TCP datagrams"
 
 
 def parse_args(argv=None):
@@ -53,6 +55,11 @@ def parse_args(argv=None):
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="c3_1500B")
+    p.add_argument("--op", choices=("csum", "verify"), default="csum",
+                   help="csum (the headline): the batch checksum, per-packet seed, complemented result; verify: "
+                        "every packet is an IPv4/TCP datagram (checksums filled by rns_tx_fill_dev, every 1009th "
+                        "corrupted) and a step is one rns_rx_verify_dev launch; at N>1 the SURVEY §8(e) leg is an "
+                        "all-reduce(sum) of the per-rank rejected-datagram counts instead of the result all-gather")
     p.add_argument("--desc", choices=("auto", "64", "32", "packed"), default="auto",
                    help="descriptor form: 64 = u64 offsets (rns_csum_batch_dev); 32 = u32 offsets "
                         "(rns_csum_batch_dev_off32); packed = u16 lengths + one offset per 64 packets "
@@ -90,6 +97,8 @@ def parse_args(argv=None):
     args = p.parse_args(argv)
     if args.shape and args.desc in ("32", "packed"):
         p.error("--shape overrides take 64-bit descriptors (--desc 64 or auto)")
+    if args.op == "verify" and (args.shape or args.desc not in ("auto", "64")):
+        p.error("--op verify takes 64-bit descriptors and the receive kernel's own shape")
     return args
 
 
@@ -251,12 +260,38 @@ class ResultGather:
         return np.concatenate([raw[r, :c] for r, c in enumerate(self.counts)])
 
 
+class BadCountReduce:
+    """SURVEY §8(e) in verify mode: the per-rank count of rejected datagrams (status
+    without RNS_RX_ACCEPT), summed over ranks with one all-reduce (RCCL on the device
+    under nccl; gloo moves a host tensor).  The count is reduced on the device first,
+    so the collective moves 8 bytes per rank."""
+
+    ACCEPT = 0x40  # RNS_RX_ACCEPT
+
+    def __init__(self, dist: Dist, device):
+        import torch
+        self.dist, self.torch = dist, torch
+        self.host_staged = dist.enabled and dist.backend != "nccl"
+        self.device = "cpu" if self.host_staged else device
+        self.total = torch.zeros(1, dtype=torch.int64, device=self.device)
+
+    def __call__(self, status):
+        torch = self.torch
+        cnt = ((status & self.ACCEPT) == 0).sum(dtype=torch.int64).view(1)
+        if self.host_staged:
+            cnt = cnt.cpu()
+        self.total.copy_(cnt)
+        if self.dist.enabled:
+            self.dist.dist.all_reduce(self.total)
+        return self.total
+
+
 # ---------------------------------------------------------------------------
 # GPU engine: the product path
 # ---------------------------------------------------------------------------
 class GpuEngine:
     def __init__(self, config: str, rank: int, local_rank: int, shape=None, steps: int = 0, world: int = 1,
-                 strong: bool = False, compact="64"):
+                 strong: bool = False, compact="64", op: str = "csum"):
         import torch
 
         from rustnetworkstack_amd.workloads import DATA_SEED, DeviceBatch, make_layout
@@ -272,6 +307,7 @@ class GpuEngine:
             # weak scaling: every rank owns a full batch of the config, with its own bytes
             return make_layout(config, data_seed=DATA_SEED + 0x1000 * rank + r)
 
+        self.op = op
         self.layout = layout(0)
         small = self.layout.arena_bytes < (512 << 20)
         # batches that fit the 256 MiB Infinity Cache are rotated so each step reads cold bytes
@@ -283,11 +319,17 @@ class GpuEngine:
             small = self.layout.arena_bytes + 16 < 2 ** 32
             jumbo = self.layout.mean_len > 2500  # pick_shape's group kernel: no wave batches, no packed form
             form = "64" if shape is not None else ("packed" if not jumbo else ("32" if small else "64"))
+        if op == "verify":  # the receive kernel reads 64-bit descriptors
+            from rustnetworkstack_amd.workloads import make_verify_batch
+            form = "64"
+            for b in self.batches:
+                make_verify_batch(b)
         self.form = form
         self.compact = form == "32"
         self.packed = form == "packed"
         for b in self.batches:  # bind every rotating batch (and upload its descriptors) before any timing
-            b.launcher(complement=True, shape=shape, compact=self.compact, packed=self.packed)
+            if op == "csum":
+                b.launcher(complement=True, shape=shape, compact=self.compact, packed=self.packed)
         self.k = 0
         self.last = self.batches[0]
         self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -303,10 +345,18 @@ class GpuEngine:
     def payload_bytes(self):
         return self.layout.payload_bytes
 
+    def _verify_call(self, b):
+        from rustnetworkstack_amd.batch import rx_verify
+        from rustnetworkstack_amd.workloads import LOCAL4, LOCAL6
+        return lambda: rx_verify(b.arena, b.off, b.length, LOCAL4, LOCAL6, status=b.status)  # current stream
+
     def step(self):
         b = self.batches[self.k % len(self.batches)]
         self.k += 1
-        b.launcher(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)()  # one ctypes call
+        if self.op == "verify":
+            self._verify_call(b)()
+        else:
+            b.launcher(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)()  # one ctypes call
         self.last = b
 
     def capture(self, steps: int, streams: int = 1):
@@ -316,9 +366,10 @@ class GpuEngine:
         stream), so consecutive steps — independent batches — may overlap on the
         device: one kernel's ramp-up under the previous one's drain."""
         torch = self.torch
-        fns = [b.rebind(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)
-               for b in self.batches]
-        del fns  # (bound once outside the capture: descriptor uploads happen here, not inside it)
+        if self.op == "csum":
+            fns = [b.rebind(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)
+                   for b in self.batches]
+            del fns  # (bound once outside the capture: descriptor uploads happen here, not inside it)
         side = [torch.cuda.Stream(device=self.device) for _ in range(max(streams, 1) - 1)]
         self.sync()
         g = torch.cuda.CUDAGraph()
@@ -331,7 +382,10 @@ class GpuEngine:
             for i in range(steps):
                 b = self.batches[i % len(self.batches)]
                 with torch.cuda.stream(lanes[i % len(lanes)]):
-                    b.rebind(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)()
+                    if self.op == "verify":
+                        self._verify_call(b)()
+                    else:
+                        b.rebind(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)()
             for s_ in side:
                 cap.wait_stream(s_)
         self.sync()
@@ -345,6 +399,21 @@ class GpuEngine:
     def step_and_gather(self):
         self.step()
         self.gather()
+
+    def reduce_bad(self):
+        """Verify mode: the all-reduce of the rejected-datagram counts of the last step's batch."""
+        return self.reducer(self.last.status)
+
+    def step_and_reduce(self):
+        self.step()
+        self.reduce_bad()
+
+    def bad_count(self) -> int:
+        """Rejected datagrams in every rotating batch after the timed steps (each verified at least once)."""
+        return sum(int(((b.status & BadCountReduce.ACCEPT) == 0).sum().item()) for b in self.batches)
+
+    def expected_bad(self) -> int:
+        return sum(b.expected_bad for b in self.batches)
 
     def per_launch_us(self, count: int) -> list:
         """`count` launches, each bracketed by its own event pair on the launch stream
@@ -377,6 +446,8 @@ class GpuEngine:
 
     def kernel_name(self) -> str:
         from rustnetworkstack_amd import _lib
+        if self.op == "verify":
+            return "csum_mixed_kernel<RX> (rns_rx_verify_dev: class-sorted data pass + header stash)"
         return _lib.load().rns_csum_shape_name(int(round(self.layout.mean_len))).decode()
 
     def out_sample(self, count: int):
@@ -535,8 +606,11 @@ def main(argv=None):
     dist = Dist()
     shape = tuple(int(x) for x in args.shape.split(",")) if args.shape else None
     strong = args.scaling == "strong" or (args.scaling == "auto" and args.config == "c5_imix")
+    verify = args.op == "verify"
+    if verify:
+        args.no_cpu_baseline = args.no_host_pipeline = True  # the headline's CPU legs; not this mode's
     engine = GpuEngine(args.config, dist.rank, dist.local_rank, shape=shape, steps=args.steps, world=dist.world,
-                       strong=strong, compact=args.desc)
+                       strong=strong, compact=args.desc, op=args.op)
     use_graph = args.graph == "on" or (args.graph == "auto" and engine.device.type == "cuda")
     if args.graph_streams <= 0:
         args.graph_streams = 3 if engine.layout.mean_len < 1000 else 2
@@ -557,15 +631,16 @@ def main(argv=None):
         ri = timed_loop(engine, _NoDist(), args.steps, 0, graph=engine.capture(args.steps, 1))
         isolated = ri["kernel_ms"] * 1e3
     per = engine.per_launch_us(args.median_launches) if args.median_launches > 0 else []
-    algo_bytes = engine.payload_bytes + 2 * engine.n
+    # payload read + the result written: u16 sum (csum) or u8 status (verify)
+    algo_bytes = engine.payload_bytes + (1 if verify else 2) * engine.n
     # descriptor bytes a launch reads (seeds included): packed 2 B length + 8 B per 64 packets
     desc_bytes = (engine.n * (2 + 2) + 8 * ((engine.n + 63) // 64) if engine.packed
-                  else engine.n * ((4 if engine.compact else 8) + 4 + 2))
+                  else engine.n * ((4 if engine.compact else 8) + 4 + (0 if verify else 2)))
     kernel_us = kernel_ms * 1e3
     achieved = algo_bytes / (kernel_us * 1e-6) / 1e9
     traffic = load_traffic(args.traffic_json, args.config)
     line = {
-        "metric": METRIC,
+        "metric": METRIC_VERIFY if verify else METRIC,
         "value": round(value, 2),
         "unit": "GiB/s",
         "n_gpus": dist.world,
@@ -580,10 +655,15 @@ def main(argv=None):
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic: splitmix64 packet bytes (seed 0x5EEDC0DE + per-rank offset), per-packet u16 seeds",
+        "data": ("synthetic: IPv4/TCP datagrams to 10.0.0.2 (splitmix64 payload, seed 0x5EEDC0DE + per-rank "
+                 "offset; checksums filled by rns_tx_fill_dev; every 1009th datagram corrupted)" if verify else
+                 "synthetic: splitmix64 packet bytes (seed 0x5EEDC0DE + per-rank offset), per-packet u16 seeds"),
         "config": {
-            "workload": f"{args.config}: {engine.n} packets x {engine.payload_bytes // max(engine.n, 1)} B per GPU, "
-                        "16 B-aligned arena in HBM, per-packet seed, complemented result (tcp.rs:970 form)",
+            "workload": (f"{args.config} verify: {engine.n} IPv4/TCP datagrams x "
+                         f"{engine.payload_bytes // max(engine.n, 1)} B per GPU, 16 B-aligned arena in HBM, "
+                         "IPv4 header + TCP checksum checked, u8 status out" if verify else
+                         f"{args.config}: {engine.n} packets x {engine.payload_bytes // max(engine.n, 1)} B per GPU, "
+                         "16 B-aligned arena in HBM, per-packet seed, complemented result (tcp.rs:970 form)"),
             "packets_per_gpu": engine.n,
             "payload_bytes_per_gpu": engine.payload_bytes,
             "batch": "one batch sharded by packet index across ranks" if strong else "a full batch per rank",
@@ -629,7 +709,24 @@ def main(argv=None):
         srt = sorted(per)
         line["roofline"]["evpair_median_us"] = round(srt[len(srt) // 2], 2)
         line["roofline"]["evpair_launches"] = len(per)
-    if dist.world > 1 and not args.no_gather:
+    if verify:
+        # every rotating batch was verified at least once (ramp / warmup / timed steps)
+        line["verify"] = {"rejected_total": int(dist.sum(float(engine.bad_count()))),
+                          "rejected_expected": int(dist.sum(float(engine.expected_bad()))),
+                          "datagrams_total": int(dist.sum(float(sum(b.layout.n for b in engine.batches))))}
+    if dist.world > 1 and not args.no_gather and verify:
+        # SURVEY §8(e), verify mode: the same steps plus one all-reduce(sum) of the per-rank rejected counts
+        engine.reducer = BadCountReduce(dist, engine.device)
+        rr = timed_loop(engine, dist, args.steps, args.warmup, step=engine.step_and_reduce)
+        rro = timed_loop(engine, dist, args.steps, args.warmup, step=engine.reduce_bad)
+        line["value_compute"] = line["value"]
+        line["value_allreduce"] = round(total_bytes / rr["elapsed_s"] / 2 ** 30, 2)
+        line["ms_per_step_allreduce"] = round(rr["elapsed_s"] * 1e3 / args.steps, 4)
+        line["allreduce_ms"] = round(rro["elapsed_s"] * 1e3 / args.steps, 4)
+        line["allreduce"] = {"collective": f"all_reduce sum ({dist.backend}) of the int64 rejected-datagram count",
+                             "bytes_per_rank": 8,
+                             "rejected_total_last_step": int(engine.reducer.total.item())}
+    elif dist.world > 1 and not args.no_gather:
         # the same steps plus one all-gather of every rank's results, and the gather alone
         engine.gatherer = ResultGather(dist, engine.n, engine.device)
         rg = timed_loop(engine, dist, args.steps, args.warmup, step=engine.step_and_gather)

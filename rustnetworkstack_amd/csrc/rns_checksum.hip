@@ -1330,7 +1330,10 @@ template <bool STRIDED, bool NT, bool BUF, bool FILL, bool RX = false, bool TX =
 #ifndef RNS_MIXED_OCC
 #define RNS_MIXED_OCC 4
 #endif
-__global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX && !TX) ? RNS_MIXED_OCC : 3) void csum_mixed_kernel(const CsumArgs a)
+#ifndef RNS_STASH_OCC  // waves/SIMD bound of the stash modes (receive verify, transmit fill/finalize)
+#define RNS_STASH_OCC 4
+#endif
+__global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX && !TX) ? RNS_MIXED_OCC : RNS_STASH_OCC) void csum_mixed_kernel(const CsumArgs a)
 {
     static_assert(int(FILL) + int(RX) + int(TX) <= 1 && !(STRIDED && (RX || TX)), "one mode at a time");
     constexpr int kMode = RX ? kStashHead : FILL ? kStashField : TX ? kStashTx : kStashNone;

@@ -185,3 +185,72 @@ class DeviceBatch:
 
     def host_out(self) -> np.ndarray:
         return self.out.view(__import__("torch").int16).cpu().numpy().view(np.uint16)
+
+
+# ---------------------------------------------------------------------------
+# Receive-verify batches (bench.py --op verify): every packet becomes an IPv4/TCP
+# datagram addressed to LOCAL4, its checksums filled by the product's own transmit
+# finalize (rns_tx_fill_dev), then every CORRUPT_EVERY-th datagram gets one payload
+# byte flipped so a known number fail (tcp.rs:544-547 drops them).
+# ---------------------------------------------------------------------------
+LOCAL4 = bytes([10, 0, 0, 2])
+REMOTE4 = bytes([10, 0, 0, 1])
+LOCAL6 = bytes.fromhex("fd000000000000000000000000000002")
+CORRUPT_EVERY, CORRUPT_FIRST = 1009, 7
+MIN_DATAGRAM = 40  # IPv4 header + TCP header
+
+
+def ipv4_tcp_headers(length: np.ndarray, src4: bytes = REMOTE4, dst4: bytes = LOCAL4) -> np.ndarray:
+    """[n, 20] IPv4 headers (IHL 5, DF, TTL 64, protocol 6, total length = the
+    datagram's length, checksum field zero) for datagrams of `length` bytes."""
+    n = int(length.shape[0])
+    h = np.zeros((n, 20), dtype=np.uint8)
+    h[:, 0] = 0x45
+    h[:, 2] = (length >> 8) & 0xFF
+    h[:, 3] = length & 0xFF
+    h[:, 6] = 0x40
+    h[:, 8] = 64
+    h[:, 9] = 6
+    h[:, 12:16] = np.frombuffer(src4, dtype=np.uint8)
+    h[:, 16:20] = np.frombuffer(dst4, dtype=np.uint8)
+    return h
+
+
+def corrupt_mask(n: int) -> np.ndarray:
+    """Datagrams whose payload byte is flipped (local packet index)."""
+    return (np.arange(n) % CORRUPT_EVERY) == CORRUPT_FIRST
+
+
+def corrupt_pos(length: np.ndarray) -> np.ndarray:
+    """Byte (from the datagram start) that corruption flips: the middle of the TCP segment."""
+    return 20 + (length.astype(np.int64) - 20) // 2
+
+
+def make_verify_batch(b: "DeviceBatch") -> None:
+    """Turn a DeviceBatch into received datagrams in place (headers written, checksums
+    filled by rns_tx_fill_dev, known corruptions applied) and give it a status array."""
+    import torch
+
+    from . import _lib
+    from .batch import tx_fill
+    lay = b.layout
+    if lay.n and int(lay.length.min()) < MIN_DATAGRAM:
+        raise ValueError(f"verify batches need datagrams of at least {MIN_DATAGRAM} B")
+    dev = b.device
+    hdr = torch.from_numpy(ipv4_tcp_headers(lay.length)).to(dev)
+    step = 1 << 20  # packets per scatter (bounds the index tensor)
+    for i in range(0, lay.n, step):
+        idx = b.off[i:i + step].view(-1, 1) + torch.arange(20, device=dev)
+        b.arena[idx.flatten()] = hdr[i:i + step].flatten()
+    st = tx_fill(b.arena, b.off, b.length)
+    want = _lib.RNS_TX_IP_FILLED | _lib.RNS_TX_L4_FILLED
+    if int((st != want).sum().item()):
+        raise RuntimeError("transmit finalize did not fill every synthetic datagram")
+    mask = corrupt_mask(lay.n)
+    sel = np.nonzero(mask)[0]
+    if sel.size:
+        pos = lay.off[sel].astype(np.int64) + corrupt_pos(lay.length[sel])
+        p = torch.from_numpy(pos).to(dev)
+        b.arena[p] ^= 0x5A
+    b.status = torch.empty(lay.n, dtype=torch.uint8, device=dev)
+    b.expected_bad = int(sel.size)

@@ -33,7 +33,9 @@ class _Batch:
 
 class CpuEngine(bench.GpuEngine):
     """Stand-in for bench.GpuEngine: same interface, oracle compute on CPU tensors."""
-    def __init__(self, config, rank, local_rank, shape=None, steps=0, world=1, strong=False, compact="64"):
+    def __init__(self, config, rank, local_rank, shape=None, steps=0, world=1, strong=False, compact="64",
+                 op="csum"):
+        assert op == "csum"
         self.torch = torch
         self.device = torch.device("cpu")
         if strong:
@@ -138,3 +140,112 @@ def test_two_rank_gloo_bench_main(tmp_path, oracle, config, n):
     for rank in (0, 1):
         assert res[rank]["counts"] == per_rank
         assert np.array_equal(np.array(res[rank]["gathered"], dtype=np.uint16), expect)
+
+
+VERIFY_WORKER = r'''
+import json, os, sys, time
+sys.path.insert(0, {root!r})
+import numpy as np
+import torch
+import bench
+from oracle import oracle as O
+from rustnetworkstack_amd import workloads as W
+
+N = {n}
+ENGINES = []
+
+class _Batch:
+    pass
+
+class CpuVerifyEngine(bench.GpuEngine):
+    """Stand-in for bench.GpuEngine in verify mode: the same datagram batch built on
+    the host (headers from workloads, checksums by the oracle's transmit restatement,
+    the same corruptions), each step = the oracle's receive restatement per datagram."""
+    def __init__(self, config, rank, local_rank, shape=None, steps=0, world=1, strong=False, compact="64",
+                 op="csum"):
+        assert op == "verify"
+        self.torch, self.op = torch, op
+        self.device = torch.device("cpu")
+        if strong:
+            self.layout = W.make_layout(config, n=N, shard=(rank, world))
+        else:
+            self.layout = W.make_layout(config, n=N, data_seed=0x5EEDC0DE + 0x1000 * rank)
+        lay = self.layout
+        arena = O.splitmix64_bytes(lay.data_seed, lay.arena_bytes)
+        hdr = W.ipv4_tcp_headers(lay.length)
+        orc = O.get_oracle()
+        self.oc = orc.compute_ones_comp
+        mask = W.corrupt_mask(lay.n)
+        pos = W.corrupt_pos(lay.length)
+        self.pkts = []
+        for i in range(lay.n):
+            o, L = int(lay.off[i]), int(lay.length[i])
+            pkt = bytearray(arena[o:o + L].tobytes())
+            pkt[:20] = hdr[i].tobytes()
+            pkt, st = O.tx_fill_ref(bytes(pkt), self.oc)
+            assert st == O.TX_IP_FILLED | O.TX_L4_FILLED
+            pkt = bytearray(pkt)
+            if mask[i]:
+                pkt[pos[i]] ^= 0x5A
+            self.pkts.append(bytes(pkt))
+        b = _Batch()
+        b.layout, b.status, b.expected_bad = lay, torch.zeros(lay.n, dtype=torch.uint8), int(mask.sum())
+        self.batches = [b]
+        self.last = b
+        self.compact, self.shape, self.k, self.timed = False, None, 0, 0
+        self.packed, self.form = False, "64"
+        self.gatherer = self.reducer = None
+        ENGINES.append(self)
+    def step(self):
+        st = [O.rx_status_ref(p, W.LOCAL4, W.LOCAL6, self.oc) for p in self.pkts]
+        self.last.status.copy_(torch.tensor(st, dtype=torch.uint8))
+    def sync(self):
+        pass
+    def begin_timing(self):
+        self.t0 = time.perf_counter()
+    def end_timing(self, steps):
+        self.ms = 1e3 * (time.perf_counter() - self.t0) / steps
+        self.timed = steps
+    def kernel_ms(self):
+        return self.ms
+    def kernel_name(self):
+        return "cpu stand-in"
+
+bench.GpuEngine = CpuVerifyEngine
+line = bench.main(["--config", {config!r}, "--op", "verify", "--steps", "2", "--warmup", "1",
+                   "--traffic-json", "/nonexistent/{{config}}.json"])
+rank = int(os.environ["RANK"])
+with open(os.path.join({outdir!r}, f"rank{{rank}}.json"), "w") as f:
+    json.dump({{"rank": rank, "line": line, "n": ENGINES[0].n, "bad": int(ENGINES[0].batches[0].expected_bad)}}, f)
+'''
+
+
+@pytest.mark.parametrize("config,n", [("c5_imix", 4001), ("c3_1500B", 2100)])
+def test_two_rank_gloo_verify_allreduce(tmp_path, config, n):
+    """Verify mode at N=2: the §8(e) all-reduce(sum) of the rejected-datagram counts
+    (one per rank) equals the corruptions planted over the whole (sharded) batch."""
+    script = tmp_path / "worker.py"
+    script.write_text(VERIFY_WORKER.format(root=ROOT, n=n, config=config, outdir=str(tmp_path)))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(script)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = {}
+    for rank in (0, 1):
+        with open(tmp_path / f"rank{rank}.json") as f:
+            res[rank] = json.load(f)
+    printed = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(printed) == 1
+    line = printed[0]
+    assert line["metric"] == __import__("bench").METRIC_VERIFY
+    bad = res[0]["bad"] + res[1]["bad"]
+    assert bad > 0
+    assert line["verify"]["rejected_expected"] == bad
+    assert line["verify"]["rejected_total"] == bad            # every corrupted datagram, and only those
+    assert line["verify"]["datagrams_total"] == res[0]["n"] + res[1]["n"]
+    assert line["allreduce"]["rejected_total_last_step"] == bad
+    for k in ("value_compute", "value_allreduce", "ms_per_step_allreduce", "allreduce_ms"):
+        assert k in line and line[k] > 0, k
+    assert "value_gather" not in line
+    assert line["cpu_baseline"] is None

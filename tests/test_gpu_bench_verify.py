@@ -1,0 +1,23 @@
+"""bench.py --op verify on the GPU (SURVEY §8(f) row 1 through the bench harness, and
+the §8(e) verify-mode count): every synthetic datagram is built on the device and
+filled by rns_tx_fill_dev, every 1009th is corrupted, and after the timed steps the
+receive kernel must have rejected exactly those (a single flipped byte always changes
+a one's-complement sum)."""
+import pytest
+
+import bench
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("config", ["c2_64B", "c3_1500B"])
+def test_bench_verify_rejects_exactly_the_corrupted(config):
+    line = bench.main(["--config", config, "--op", "verify", "--steps", "12", "--warmup", "1", "--ramp-s", "0",
+                       "--traffic-json", "/nonexistent/{config}.json"])
+    v = line["verify"]
+    assert v["rejected_expected"] > 0
+    assert v["rejected_total"] == v["rejected_expected"]
+    assert line["metric"] == bench.METRIC_VERIFY
+    assert line["roofline"]["kernel"].startswith("csum_mixed_kernel<RX>")
+    assert 0 < line["roofline"]["frac"] < 1.0
+    assert line["cpu_baseline"] is None
