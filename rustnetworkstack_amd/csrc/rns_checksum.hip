@@ -1123,6 +1123,13 @@ __device__ __forceinline__ uint32_t wave_class_pass(const CsumArgs &a, __amdgpu_
 // trimmed packet pairs them.  The L4 seed is the pseudo-header sum with dest = the
 // LOCAL address, as the reference passes netif::get_ipaddr().
 // ---------------------------------------------------------------------------
+// A/B knob: receive verify's owner-lane finish takes a short path for 16-byte-aligned
+// datagrams (header dwords as stashed; a 20-byte IPv4 header summed without byte masks).
+#ifndef RNS_RX_ALIGNED_FAST
+#define RNS_RX_ALIGNED_FAST 1
+#endif
+constexpr bool kRxAlignedFast = RNS_RX_ALIGNED_FAST != 0;
+
 enum : uint32_t {
     kMetaV4 = 1, kMetaV6 = 2, kMetaFrag = 4, kMetaMalformed = 8,
     kMetaL4Checked = 16, kMetaUnchecked = 32, kMetaUnknown = 64,
@@ -1523,13 +1530,29 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX
                 ch[i] = mine_st[i];
             const uint32_t s = static_cast<uint32_t>(d_start & 15);
             uint32_t head[6];
-            head_from_stash(ch, s, head);
+            if (kRxAlignedFast && s == 0) {  // 16-byte-aligned datagram: the dwords as they are
+                const uint32_t w6[6] = {ch[0].x, ch[0].y, ch[0].z, ch[0].w, ch[1].x, ch[1].y};
+#pragma unroll
+                for (int k = 0; k < 6; ++k)
+                    head[k] = w6[k];
+            } else {
+                head_from_stash(ch, s, head);
+            }
             const RxParse rp = (live && d_len != 0) ? rx_parse(head, d_len, a.local4_sum, a.local6_sum)
                                                     : RxParse{kMetaMalformed, 0u, 0u};
             uint32_t hdr_res = 0, l4_res = 0;
             if (!(rp.meta & kMetaMalformed)) {
                 const int hlo = static_cast<int>(s), hhi = hlo + static_cast<int>(rp.hdr);  // <= 15 + 60
-                uint32_t H = stash_sum_le(ch, hlo, hhi);
+                uint32_t H;
+                if (kRxAlignedFast && hlo == 0 && hhi == 20) {  // aligned IPv4 header, no options: 5 dwords
+                    H = __builtin_amdgcn_sad_u16(ch[0].x, 0, 0u);
+                    H = __builtin_amdgcn_sad_u16(ch[0].y, 0, H);
+                    H = __builtin_amdgcn_sad_u16(ch[0].z, 0, H);
+                    H = __builtin_amdgcn_sad_u16(ch[0].w, 0, H);
+                    H = __builtin_amdgcn_sad_u16(ch[1].x, 0, H);
+                } else {
+                    H = stash_sum_le(ch, hlo, hhi);
+                }
                 uint4 tail[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
                 if (hhi > 48) {  // IPv6 past offset 8, IPv4 with options: header bytes in chunks 3-4
                     tail[0] = mine_st[3];
@@ -2358,7 +2381,13 @@ int rns_rx_verify_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64
     a.local6_sum = be_sum(local_ipv6, 16);
     const uint64_t waves = (static_cast<uint64_t>(n) + 63) / 64;  // 64 datagrams per wave
     constexpr int BLK = kMixedBlock<true>;
-    const dim3 grid(static_cast<uint32_t>((waves + BLK / 64 - 1) / (BLK / 64))), block(BLK);
+    uint64_t blocks = (waves + BLK / 64 - 1) / (BLK / 64);
+#ifndef RNS_RX_GRID_CAP  // A/B knob: at most this many workgroups (waves loop over batches); 0 = none
+#define RNS_RX_GRID_CAP 0
+#endif
+    if (RNS_RX_GRID_CAP != 0 && blocks > RNS_RX_GRID_CAP)
+        blocks = RNS_RX_GRID_CAP;
+    const dim3 grid(static_cast<uint32_t>(blocks)), block(BLK);
     hipStream_t st = static_cast<hipStream_t>(stream);
 #ifdef RNS_RX_PLAIN
     constexpr bool kNT = false;
