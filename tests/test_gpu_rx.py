@@ -168,3 +168,19 @@ def test_full_size_tcp_batch_verifies_and_catches_corruption():
     assert np.array_equal(st, exp)
     del b
     torch.cuda.empty_cache()
+
+
+def test_tiny_datagrams_capped_grid_every_status():
+    """ACK-sized datagrams (arena bytes per datagram <= 128) run on a capped grid whose
+    waves loop over several 64-datagram batches: every status must still be exact —
+    accepted, or (the planted corruptions, one TCP byte flipped) IP-only."""
+    from rustnetworkstack_amd.workloads import LOCAL4, LOCAL6, corrupt_mask, make_verify_batch
+    n = 4096 * 64 * 2 + 123            # > 2 batches per wave of the 4096-wave cap, ragged tail
+    lay = make_layout("d40B", n=n)
+    b = DeviceBatch(lay, DEV)
+    make_verify_batch(b)
+    assert lay.arena_bytes // n <= 128
+    st = rx_verify(b.arena, b.off, b.length, LOCAL4, LOCAL6).cpu().numpy()
+    want = np.full(n, _lib.RNS_RX_ACCEPT | _lib.RNS_RX_IP_OK | _lib.RNS_RX_L4_OK, dtype=np.uint8)
+    want[corrupt_mask(n)] = _lib.RNS_RX_IP_OK
+    assert np.array_equal(st, want)
