@@ -842,6 +842,22 @@ __device__ __forceinline__ FillSite fill_site(const CsumArgs &a, uint64_t d_star
     return f;
 }
 
+// A/B knob: the transmit stores with the nontemporal cache policy.
+#ifndef RNS_FILL_NTSTORE
+#define RNS_FILL_NTSTORE 0
+#endif
+__device__ __forceinline__ void store_block(uint4 *p, uint4 v)
+{
+    if constexpr (RNS_FILL_NTSTORE != 0) {
+        __builtin_nontemporal_store(v.x, &p->x);
+        __builtin_nontemporal_store(v.y, &p->y);
+        __builtin_nontemporal_store(v.z, &p->z);
+        __builtin_nontemporal_store(v.w, &p->w);
+    } else {
+        *p = v;
+    }
+}
+
 // set_be16(&mut header[f..f+2], checksum): rewrite the block from the stash (stp =
 // the packet's stash chunks) with the field patched in, or store the two bytes.
 __device__ __forceinline__ void fill_store(const CsumArgs &a, const FillSite &f, uint64_t d_start, uint32_t d_field,
@@ -869,7 +885,7 @@ __device__ __forceinline__ void fill_store(const CsumArgs &a, const FillSite &f,
                         if (bpos < 16 && d == (bpos >> 2))
                             w[d] = (w[d] & ~(0xffu << sh)) | (byte << sh);
                 }
-                *reinterpret_cast<uint4 *>(arena_w + f.blk + 16 * i) = make_uint4(w[0], w[1], w[2], w[3]);
+                store_block(reinterpret_cast<uint4 *>(arena_w + f.blk + 16 * i), make_uint4(w[0], w[1], w[2], w[3]));
             }
         }
     } else {
@@ -1509,8 +1525,8 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX
                                    (fpos - 16u * static_cast<uint32_t>(lo)) != 31u;
                 if (whole) {
                     uint4 *sp = reinterpret_cast<uint4 *>(arena_w + sec);
-                    sp[0] = own[lo];
-                    sp[1] = own[lo + 1];
+                    store_block(sp, own[lo]);
+                    store_block(sp + 1, own[lo + 1]);
                 } else {
                     arena_w[d_start + fld[k]] = static_cast<uint8_t>(val[k] >> 8);
                     arena_w[d_start + fld[k] + 1] = static_cast<uint8_t>(val[k]);
