@@ -86,9 +86,10 @@ def parse_args(argv=None):
                         "profiles/r02_graph_overlap.json); auto = on (every rank, so N=1 and N>1 are timed alike)")
     p.add_argument("--graph-streams", type=int, default=0,
                    help="graph mode: steps alternate over this many streams (independent batches may overlap); "
-                        "0 = auto: 3 for batches of small packets (mean < 1000 B: c2 11.35 -> 11.10 us, IMIX "
-                        "493 -> 481-486 us), 2 otherwise (c3: 229.5 with 2, 231-232 with 3; profiles/"
-                        "r02_graph_overlap.json)")
+                        "0 = auto: 3 for tiny packets (mean < 128 B: c2 11.15-11.19 us with 3, 11.2-11.5 with 2 or 4), "
+                        "4 for small mixed packets (mean < 1000 B: IMIX 405-424 us with 4, 422-430 with 3, 450-480 "
+                        "with 2), 2 otherwise (c3 and c4 equal for 2-6; profiles/r02_graph_overlap.json, "
+                        "r02_graph_streams.json)")
     p.add_argument("--scaling", choices=("auto", "weak", "strong"), default="auto",
                    help="weak: every rank checksums a full batch of the config; strong: the config's batch is "
                         "sharded by packet index across ranks (auto: strong for c5_imix, whose BASELINE.json "
@@ -613,7 +614,8 @@ def main(argv=None):
                        strong=strong, compact=args.desc, op=args.op)
     use_graph = args.graph == "on" or (args.graph == "auto" and engine.device.type == "cuda")
     if args.graph_streams <= 0:
-        args.graph_streams = 3 if engine.layout.mean_len < 1000 else 2
+        mean = engine.layout.mean_len
+        args.graph_streams = 3 if mean < 128 else 4 if mean < 1000 else 2
     graph = engine.capture(args.steps, args.graph_streams) if use_graph else None
     ramp_steps = clock_ramp(engine, args.ramp_s, graph=graph) if args.ramp_s > 0 else 0
     r = timed_loop(engine, dist, args.steps, args.warmup, graph=graph)
