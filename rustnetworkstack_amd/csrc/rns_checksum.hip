@@ -2335,6 +2335,27 @@ int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
     return hip_status(hipGetLastError());
 }
 
+// Grid of the stash-mode kernels (one 64-datagram batch per one-wave workgroup).  Batches
+// of tiny datagrams (arena bytes per datagram <= 128: ACK-sized) run on a capped grid, each
+// wave looping over several batches: one-batch waves are mostly launch ramp there (64 B
+// verify 18.9 -> 17.2-17.8 us per step); larger datagrams keep one wave per batch (a cap
+// measured 3-6 % slower on IMIX; profiles/r02_rx_cap_ab.json).
+#ifndef RNS_RX_GRID_CAP  // A/B knob: the cap for tiny datagrams; 0 = none
+#define RNS_RX_GRID_CAP 4096
+#endif
+// Receive verify and transmit finalize take the cap (64 B finalize 35.2-36.3 -> 33.3 us);
+// the single-field fill does not (64 B fill 28.9-29.2 us without, 29.8-30.0 with it:
+// profiles/r02_tx_cap_ab.json).
+static uint64_t stash_blocks(uint64_t n, uint64_t arena_bytes, bool tiny_cap)
+{
+    constexpr int BLK = kMixedBlock<true>;
+    uint64_t blocks = ((n + 63) / 64 + BLK / 64 - 1) / (BLK / 64);
+    const bool cap = RNS_RX_GRID_CAP != 0 && tiny_cap && arena_bytes / n <= 128;
+    if (cap && blocks > RNS_RX_GRID_CAP)
+        blocks = RNS_RX_GRID_CAP;
+    return blocks;
+}
+
 int rns_csum_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off, const uint32_t *d_len,
                       const uint16_t *d_seed, const uint16_t *d_field, uint32_t field_off, uint16_t *d_out,
                       uint32_t n, uint32_t flags, uint32_t *d_bad, void *stream)
@@ -2357,8 +2378,7 @@ int rns_csum_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_
     a.field = d_field;
     a.field_off = field_off;
     constexpr int BLK = kMixedBlock<true>;
-    const uint64_t blocks = ((static_cast<uint64_t>(n) + 63) / 64 + BLK / 64 - 1) / (BLK / 64);
-    const dim3 grid(static_cast<uint32_t>(blocks)), block(BLK);
+    const dim3 grid(static_cast<uint32_t>(stash_blocks(n, arena_bytes, false))), block(BLK);
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (buf_records(a) < kOobOffset)
         hipLaunchKernelGGL((csum_mixed_kernel<false, false, true, true>), grid, block, 0, st, a);
@@ -2397,17 +2417,8 @@ int rns_rx_verify_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64
     a.local6_sum = be_sum(local_ipv6, 16);
     const uint64_t waves = (static_cast<uint64_t>(n) + 63) / 64;  // 64 datagrams per wave
     constexpr int BLK = kMixedBlock<true>;
-    uint64_t blocks = (waves + BLK / 64 - 1) / (BLK / 64);
-    // Batches of tiny datagrams (arena bytes per datagram <= 128: ACK-sized) run on a
-    // capped grid, each wave looping over several batches: one-batch waves are mostly
-    // launch ramp there (64 B datagrams 18.9 -> 17.2-17.8 us per step); larger datagrams
-    // keep one wave per batch (a cap measured 3-6 % slower on IMIX; profiles/r02_rx_cap_ab.json).
-#ifndef RNS_RX_GRID_CAP  // A/B knob: the cap for tiny datagrams; 0 = none
-#define RNS_RX_GRID_CAP 4096
-#endif
-    if (RNS_RX_GRID_CAP != 0 && arena_bytes / n <= 128 && blocks > RNS_RX_GRID_CAP)
-        blocks = RNS_RX_GRID_CAP;
-    const dim3 grid(static_cast<uint32_t>(blocks)), block(BLK);
+    (void)waves;
+    const dim3 grid(static_cast<uint32_t>(stash_blocks(n, arena_bytes, true))), block(BLK);
     hipStream_t st = static_cast<hipStream_t>(stream);
 #ifdef RNS_RX_PLAIN
     constexpr bool kNT = false;
@@ -2438,8 +2449,7 @@ int rns_tx_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_of
     a.flags = RNS_FLAG_COMPLEMENT;
     a.status = d_status;
     constexpr int BLK = kMixedBlock<true>;
-    const uint64_t waves = (static_cast<uint64_t>(n) + 63) / 64;  // 64 datagrams per wave
-    const dim3 grid(static_cast<uint32_t>((waves + BLK / 64 - 1) / (BLK / 64))), block(BLK);
+    const dim3 grid(static_cast<uint32_t>(stash_blocks(n, arena_bytes, true))), block(BLK);
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (buf_records(a) < kOobOffset)
         hipLaunchKernelGGL((csum_mixed_kernel<false, false, true, false, false, true>), grid, block, 0, st, a);

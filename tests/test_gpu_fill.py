@@ -118,3 +118,25 @@ def test_field_out_of_packet_is_rejected():
     assert int(bad.item()) == 2          # 16+2 > 17, and 40+30 > 64
     assert np.array_equal(arena.cpu().numpy(), before)
     assert list(host_u16(out)) == [0, 0]
+
+
+def test_tiny_packets_capped_grid_fill_every_packet(oracle):
+    """64-byte segments (arena bytes per packet <= 128) take the capped grid whose waves
+    loop over several 64-packet batches: every packet's stored field must still be the
+    oracle's, and every packet must pass the receive check afterwards."""
+    n = 4096 * 64 * 2 + 77
+    lay = make_layout("c2_64B", n=n)
+    b = DeviceBatch(lay, DEV)
+    assert lay.arena_bytes // n <= 128
+    before = b.arena[:lay.arena_bytes].cpu().numpy()
+    out = torch.empty(n, dtype=torch.uint16, device=DEV)
+    csum_fill(b.arena, b.off, b.length, b.seed, field_off=16, out=out)
+    rx = csum_batch(b.arena, b.off, b.length, b.seed, complement=True)
+    assert int((rx.view(torch.int16) != 0).sum().item()) == 0
+    field = np.full(n, 16, dtype=np.uint32)
+    _, expect = expected_fill(oracle, before, lay.off, lay.length, lay.seed, field)
+    after = b.arena[:lay.arena_bytes].cpu().numpy()
+    assert np.array_equal(stored_be(after, lay.off, field), expect)
+    assert np.array_equal(host_u16(out), expect)
+    del b
+    torch.cuda.empty_cache()
