@@ -332,6 +332,7 @@ class GpuEngine:
             if op == "csum":
                 b.launcher(complement=True, shape=shape, compact=self.compact, packed=self.packed)
         self.k = 0
+        self.used = set()  # indices of the rotating batches some step has run on
         self.last = self.batches[0]
         self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         self.timed = 0
@@ -353,6 +354,7 @@ class GpuEngine:
 
     def step(self):
         b = self.batches[self.k % len(self.batches)]
+        self.used.add(self.k % len(self.batches))
         self.k += 1
         if self.op == "verify":
             self._verify_call(b)()
@@ -382,6 +384,7 @@ class GpuEngine:
             lanes = [cap] + side
             for i in range(steps):
                 b = self.batches[i % len(self.batches)]
+                self.used.add(i % len(self.batches))
                 with torch.cuda.stream(lanes[i % len(lanes)]):
                     if self.op == "verify":
                         self._verify_call(b)()
@@ -409,12 +412,16 @@ class GpuEngine:
         self.step()
         self.reduce_bad()
 
+    def verified_batches(self):
+        """The rotating batches some step has verified (K < the rotation leaves some untouched)."""
+        return [self.batches[i] for i in sorted(self.used)]
+
     def bad_count(self) -> int:
-        """Rejected datagrams in every rotating batch after the timed steps (each verified at least once)."""
-        return sum(int(((b.status & BadCountReduce.ACCEPT) == 0).sum().item()) for b in self.batches)
+        """Rejected datagrams in the verified batches after the timed steps."""
+        return sum(int(((b.status & BadCountReduce.ACCEPT) == 0).sum().item()) for b in self.verified_batches())
 
     def expected_bad(self) -> int:
-        return sum(b.expected_bad for b in self.batches)
+        return sum(b.expected_bad for b in self.verified_batches())
 
     def per_launch_us(self, count: int) -> list:
         """`count` launches, each bracketed by its own event pair on the launch stream
@@ -715,7 +722,7 @@ def main(argv=None):
         # every rotating batch was verified at least once (ramp / warmup / timed steps)
         line["verify"] = {"rejected_total": int(dist.sum(float(engine.bad_count()))),
                           "rejected_expected": int(dist.sum(float(engine.expected_bad()))),
-                          "datagrams_total": int(dist.sum(float(sum(b.layout.n for b in engine.batches))))}
+                          "datagrams_total": int(dist.sum(float(sum(b.layout.n for b in engine.verified_batches()))))}
     if dist.world > 1 and not args.no_gather and verify:
         # SURVEY §8(e), verify mode: the same steps plus one all-reduce(sum) of the per-rank rejected counts
         engine.reducer = BadCountReduce(dist, engine.device)

@@ -193,7 +193,7 @@ class CpuVerifyEngine(bench.GpuEngine):
         self.batches = [b]
         self.last = b
         self.compact, self.shape, self.k, self.timed = False, None, 0, 0
-        self.packed, self.form = False, "64"
+        self.packed, self.form, self.used = False, "64", {{0}}
         self.gatherer = self.reducer = None
         ENGINES.append(self)
     def step(self):

@@ -10,13 +10,15 @@ import bench
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("config", ["c2_64B", "c3_1500B"])
-def test_bench_verify_rejects_exactly_the_corrupted(config):
-    line = bench.main(["--config", config, "--op", "verify", "--steps", "12", "--warmup", "1", "--ramp-s", "0",
+@pytest.mark.parametrize("config,steps", [("c2_64B", 12), ("c2_64B", 5), ("c3_1500B", 12)])
+def test_bench_verify_rejects_exactly_the_corrupted(config, steps):
+    """(c2 rotates 12 batches: 5 steps leave some unverified, and only the verified ones count.)"""
+    line = bench.main(["--config", config, "--op", "verify", "--steps", str(steps), "--warmup", "1", "--ramp-s", "0",
                        "--traffic-json", "/nonexistent/{config}.json"])
     v = line["verify"]
     assert v["rejected_expected"] > 0
     assert v["rejected_total"] == v["rejected_expected"]
+    assert v["datagrams_total"] > 0
     assert line["metric"] == bench.METRIC_VERIFY
     assert line["roofline"]["kernel"].startswith("csum_mixed_kernel<RX>")
     assert 0 < line["roofline"]["frac"] < 1.0
