@@ -90,6 +90,10 @@ def parse_args(argv=None):
                         "4 for small mixed packets (mean < 1000 B: IMIX 405-424 us with 4, 422-430 with 3, 450-480 "
                         "with 2), 2 otherwise (c3 and c4 equal for 2-6; profiles/r02_graph_overlap.json, "
                         "r02_graph_streams.json)")
+    p.add_argument("--shard", default="",
+                   help="r/N: one GPU runs rank r's packet-index shard of the config's batch as an N-rank strong-scaling "
+                        "run would cut it (make_layout(config, shard=(r, N))) — the per-rank workload of the N-GPU "
+                        "point measured on one GPU; the line adds the shard's all-gather payload as a separate leg")
     p.add_argument("--scaling", choices=("auto", "weak", "strong"), default="auto",
                    help="weak: every rank checksums a full batch of the config; strong: the config's batch is "
                         "sharded by packet index across ranks (auto: strong for c5_imix, whose BASELINE.json "
@@ -100,7 +104,23 @@ def parse_args(argv=None):
         p.error("--shape overrides take 64-bit descriptors (--desc 64 or auto)")
     if args.op == "verify" and (args.shape or args.desc not in ("auto", "64")):
         p.error("--op verify takes 64-bit descriptors and the receive kernel's own shape")
+    args.shard_rw = None
+    if args.shard:
+        try:
+            r_, n_ = (int(x) for x in args.shard.split("/"))
+        except ValueError:
+            p.error("--shard takes r/N, e.g. 7/8")
+        if not (n_ >= 1 and 0 <= r_ < n_):
+            p.error("--shard r/N needs 0 <= r < N")
+        args.shard_rw = (r_, n_)
     return args
+
+
+def auto_graph_streams(mean_len: float) -> int:
+    """Streams the graph-mode timed steps alternate over (profiles/r02_graph_streams.json, and
+    r03 with every concurrently running step reading its own batch): 3 for tiny packets, 4 for
+    small mixed ones, 2 for MTU and jumbo batches."""
+    return 3 if mean_len < 128 else 4 if mean_len < 1000 else 2
 
 
 # ---------------------------------------------------------------------------
@@ -292,13 +312,16 @@ class BadCountReduce:
 # ---------------------------------------------------------------------------
 class GpuEngine:
     def __init__(self, config: str, rank: int, local_rank: int, shape=None, steps: int = 0, world: int = 1,
-                 strong: bool = False, compact="64", op: str = "csum"):
+                 strong: bool = False, compact="64", op: str = "csum", min_batches: int = 1, shard=None):
         import torch
 
         from rustnetworkstack_amd.workloads import DATA_SEED, DeviceBatch, make_layout
         self.torch = torch
         self.device = torch.device(f"cuda:{local_rank}")
         torch.cuda.set_device(self.device)
+
+        if shard is not None:  # --shard r/N on one process: rank r of an N-rank strong-scaling run
+            rank, world, strong = shard[0], shard[1], True
 
         def layout(r):
             if strong:  # this rank's packet-index shard of the one batch (same sizes and seeds on every rank)
@@ -311,8 +334,14 @@ class GpuEngine:
         self.op = op
         self.layout = layout(0)
         small = self.layout.arena_bytes < (512 << 20)
-        # batches that fit the 256 MiB Infinity Cache are rotated so each step reads cold bytes
+        # Rotating batches, each with its own bytes (cache honesty):
+        #  * batches that fit the 256 MiB Infinity Cache rotate so each step reads cold bytes
+        #    (>= 768 MiB between two reads of one batch);
+        #  * at least one batch per graph stream (min_batches), so no two steps that may run
+        #    at the same time read the same arena — a follower dispatch a few tens of us
+        #    behind another over the SAME bytes would be served from the Infinity Cache.
         nrot = max(1, -(-(768 << 20) // max(self.layout.arena_bytes, 1))) if small else 1
+        nrot = max(nrot, int(min_batches))
         self.batches = [DeviceBatch(self.layout if r == 0 else layout(r), self.device) for r in range(nrot)]
         self.shape = shape
         form = {True: "32", False: "64"}.get(compact, compact)
@@ -589,6 +618,47 @@ def host_pipeline_rate(engine: GpuEngine) -> dict:
             "matches_device_resident": exact}
 
 
+def shard_leg(engine, args) -> dict:
+    """--shard r/N: what the N-rank strong-scaling run adds to this rank's compute — the
+    SURVEY §8(e) all-gather of the u16 results (2 B per packet of the WHOLE batch land on
+    every rank).  A one-GPU box has no peer for the RCCL all-gather itself, so this leg
+    reports its payload and the time of a local HBM copy of the same bytes (a floor for
+    writing them; the xGMI collective is what the driver's N-GPU run times as gather_ms)."""
+    import torch
+
+    from rustnetworkstack_amd.workloads import make_layout
+    r_, n_ = args.shard_rw
+    whole = make_layout(args.config)
+    recv_bytes = 2 * whole.n
+    per_rank = 2 * (-(-whole.n // n_))
+    src = torch.empty(recv_bytes, dtype=torch.uint8, device=engine.device)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 20
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize()
+    copy_us = 1e3 * e0.elapsed_time(e1) / reps
+    return {"rank": r_, "world": n_, "packets": engine.n, "payload_bytes": engine.payload_bytes,
+            "batch_packets": whole.n, "batch_payload_bytes": whole.payload_bytes,
+            "share_of_batch_bytes": round(engine.payload_bytes / whole.payload_bytes, 5),
+            "gather": {"collective": "all_gather of uint8 results (2 B per packet), run by the N-GPU driver bench",
+                       "bytes_sent_per_rank": per_rank, "bytes_received_per_rank": per_rank * (n_ - 1),
+                       "bytes_resident_after_per_rank": recv_bytes,
+                       "local_copy_us": round(copy_us, 2),
+                       "local_copy_what": f"device-to-device copy of {recv_bytes} B in this GPU's HBM "
+                                          "(no peer GPU on a 1-GPU box), mean of 20"}}
+
+
+def _gpu_available() -> bool:
+    import torch
+    return torch.cuda.is_available()
+
+
 class _NoDist:
     """Single-process stand-in for Dist (the isolated re-measurement needs no barrier)."""
     enabled = False
@@ -617,12 +687,17 @@ def main(argv=None):
     verify = args.op == "verify"
     if verify:
         args.no_cpu_baseline = args.no_host_pipeline = True  # the headline's CPU legs; not this mode's
-    engine = GpuEngine(args.config, dist.rank, dist.local_rank, shape=shape, steps=args.steps, world=dist.world,
-                       strong=strong, compact=args.desc, op=args.op)
-    use_graph = args.graph == "on" or (args.graph == "auto" and engine.device.type == "cuda")
+    if args.shard_rw is not None and dist.world > 1:
+        raise SystemExit("--shard r/N is a one-process measurement of one rank's shard (use --scaling strong at N>1)")
+    if args.shard_rw is not None:
+        strong = True
+    use_graph = args.graph == "on" or (args.graph == "auto" and _gpu_available())
     if args.graph_streams <= 0:
-        mean = engine.layout.mean_len
-        args.graph_streams = 3 if mean < 128 else 4 if mean < 1000 else 2
+        from rustnetworkstack_amd.workloads import make_layout
+        args.graph_streams = auto_graph_streams(make_layout(args.config, n=4096).mean_len)
+    engine = GpuEngine(args.config, dist.rank, dist.local_rank, shape=shape, steps=args.steps, world=dist.world,
+                       strong=strong, compact=args.desc, op=args.op,
+                       min_batches=args.graph_streams if use_graph else 1, shard=args.shard_rw)
     graph = engine.capture(args.steps, args.graph_streams) if use_graph else None
     ramp_steps = clock_ramp(engine, args.ramp_s, graph=graph) if args.ramp_s > 0 else 0
     r = timed_loop(engine, dist, args.steps, args.warmup, graph=graph)
@@ -683,6 +758,9 @@ def main(argv=None):
                             "packed": "packed: u16 length + u16 seed per packet, u64 offset per 64 packets "
                                       "(rns_csum_batch_packed_dev)"}[engine.form],
             "rotating_batches": len(engine.batches),
+            "rotation": ("one batch per graph stream at least, each with its own bytes: steps that may run at the same "
+                         "time never read the same arena" if use_graph and args.graph_streams > 1 else
+                         "batches below 512 MiB rotate over >= 768 MiB of arenas"),
             "launch": (f"one HIP graph of the {args.steps} step launches (torch.cuda.CUDAGraph) over "
                        f"{args.graph_streams} stream(s), replayed once" if use_graph else "one C-ABI call per step"),
         },
@@ -707,6 +785,13 @@ def main(argv=None):
         },
         "cpu_baseline": None,
     }
+    if args.shard_rw is not None:
+        line["shard"] = shard_leg(engine, args)
+        line["config"]["workload"] = (f"{args.config} shard {args.shard_rw[0]}/{args.shard_rw[1]} (one rank's packet-index "
+                                      f"range of the config's batch, measured alone on one GPU): "
+                                      + line["config"]["workload"].split(": ", 1)[1])
+        line["config"]["batch"] = (f"rank {args.shard_rw[0]}'s shard of one batch sharded by packet index across "
+                                   f"{args.shard_rw[1]} ranks")
     if isolated is not None:
         line["roofline"]["isolated"] = {
             "kernel_avg_us": round(isolated, 2),

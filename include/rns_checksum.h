@@ -185,7 +185,7 @@ int rns_csum_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_
 /* Receive verify (§8f row 1): for each received IP datagram
  * d_arena[d_off[i] .. + d_len[i]), the checks the stack applies before handing it
  * to the transport layer — ip_input_v4 header checksum (ip.rs:76-80), fragment
- * drop (ip.rs:84-87), protocol dispatch (ip.rs:117-128), TCP validate_checksum
+ * drop (ip.rs:84-87), protocol dispatch (ip.rs:123-131), TCP validate_checksum
  * with the pseudo-header built from the source address and the LOCAL address
  * (tcp.rs:838-850), ICMPv4 (icmp.rs:46-50), ICMPv6 (icmp.rs:62-75); UDP is not
  * verified by the stack (udp.rs:126-148).  As in the reference, the L4 length is

@@ -96,8 +96,8 @@ def rx_verify_ref(pkt: bytes, local4: bytes, local6: bytes, ones_comp=None) -> t
 
     ip_input (ip.rs:38-48) -> ip_input_v4 (ip.rs:65-92: header checksum over
     header[..IHL*4], fragment drop, protocol header[9], source header[12..16],
-    trim_head(IHL*4)) / ip_input_v6 (ip.rs:108-115: protocol header[6], source
-    header[8..24], trim_head(40)) -> ip_input_common (ip.rs:117-128) -> tcp_input's
+    trim_head(IHL*4)) / ip_input_v6 (ip.rs:114-121: protocol header[6], source
+    header[8..24], trim_head(40)) -> ip_input_common (ip.rs:123-131) -> tcp_input's
     validate_checksum (tcp.rs:838-850: pseudo-header with dest = local address of
     the source's family, length = remaining buffer length), icmp_input_v4
     (icmp.rs:44-50: no pseudo-header), icmp_input_v6 (icmp.rs:62-75: dest = local

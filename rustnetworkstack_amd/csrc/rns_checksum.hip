@@ -1127,8 +1127,8 @@ __device__ __forceinline__ uint32_t wave_class_pass(const CsumArgs &a, __amdgpu_
 
 // ---------------------------------------------------------------------------
 // Receive verify (§8f row 1), fused into the mixed kernel (kStashHead): the checks
-// ip_input_v4 (ip.rs:65-92), ip_input_v6 (ip.rs:108-115), ip_input_common
-// (ip.rs:117-128), tcp::validate_checksum (tcp.rs:838-850), icmp_input_v4
+// ip_input_v4 (ip.rs:65-92), ip_input_v6 (ip.rs:114-121), ip_input_common
+// (ip.rs:123-131), tcp::validate_checksum (tcp.rs:838-850), icmp_input_v4
 // (icmp.rs:44-50) and icmp_input_v6 (icmp.rs:62-75) apply to a received datagram.
 // A wave takes 64 datagrams, one per owner lane.  The data pass is the plain one
 // over the WHOLE datagram (its LE word sum T); the lanes that load a datagram's
@@ -1239,8 +1239,8 @@ __device__ __forceinline__ RxParse rx_parse(const uint32_t (&h)[6], uint32_t L, 
         if (L < 40)                                          // trim_head(IPV6_HEADER_LEN) would panic
             return r;
         r.meta = kMetaV6;
-        proto = p(6);                                        // ip.rs:110
-        for (int k = 8; k < 24; k += 2)                      // source address, ip.rs:111
+        proto = p(6);                                        // ip.rs:116
+        for (int k = 8; k < 24; k += 2)                      // source address, ip.rs:117
             src_sum += p(k) << 8 | p(k + 1);
     } else {
         return r;                                            // "IP: Invalid version field"
@@ -1262,7 +1262,7 @@ __device__ __forceinline__ RxParse rx_parse(const uint32_t (&h)[6], uint32_t L, 
     } else if (proto == 17) {
         r.meta |= kMetaUnchecked;                            // udp.rs:126-148 never verifies
     } else {
-        r.meta |= kMetaUnknown;                              // ip.rs:126 "Unknown protocol"
+        r.meta |= kMetaUnknown;                              // ip.rs:129 "Unknown protocol"
     }
     return r;
 }

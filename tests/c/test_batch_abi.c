@@ -18,6 +18,11 @@
 #include "rns_checksum.h"
 
 int32_t oracle_compute_ones_comp(uint16_t in_checksum, const uint8_t *slice, size_t len);
+int32_t oracle_compute_checksum(const uint8_t *slice, size_t len);
+int32_t oracle_compute_pseudo_header_checksum(const uint8_t *src, size_t src_len, const uint8_t *dst, size_t dst_len,
+                                              uint64_t length, uint8_t protocol);
+void oracle_chain_batch(const uint8_t *arena, const uint64_t *frag_off, const uint32_t *frag_len, const uint32_t *first,
+                        const uint16_t *seed, uint16_t *out, size_t npkts, int complement);
 
 static uint64_t rng_state = 0x5EEDC0DEull;
 static uint64_t next_u64(void)
@@ -47,6 +52,252 @@ static int failures = 0;
             return 2;                                                                              \
         }                                                                                          \
     } while (0)
+
+static void fill_random(uint8_t *p, uint64_t bytes)
+{
+    for (uint64_t b = 0; b < bytes; b += 8) {
+        const uint64_t w = next_u64();
+        memcpy(p + b, &w, bytes - b < 8 ? bytes - b : 8);
+    }
+}
+
+/* rns_csum_batch_packed_dev (util.rs:88-110 per packet, offsets implied by the lengths):
+ * lengths 1..1600 plus some jumbo ones, packed at 16-byte alignment by rns_packed_layout,
+ * 7 (non-multiple-of-64) packets past a whole number of blocks. */
+static int test_packed(hipStream_t st)
+{
+    const uint32_t n = 64 * 300 + 7;
+    uint16_t *len16 = malloc(n * sizeof *len16), *seed = malloc(n * sizeof *seed);
+    uint16_t *want = malloc(n * sizeof *want), *got = malloc(n * sizeof *got);
+    uint64_t *off = malloc(n * sizeof *off), *blk = malloc(((n + 63) / 64) * sizeof *blk), end = 0;
+    uint32_t *len32 = malloc(n * sizeof *len32);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t r = next_u64();
+        len16[i] = (uint16_t)((i % 101 == 0) ? 9000u : 1u + (uint32_t)(r % 1600u));
+        len32[i] = len16[i];
+        seed[i] = (uint16_t)(r >> 32);
+    }
+    CHECK(rns_packed_layout(len16, n, 4, 48, blk, off, &end) == RNS_OK, "rns_packed_layout");
+    const uint64_t bytes = end + 16;
+    uint8_t *arena = malloc(bytes);
+    fill_random(arena, bytes);
+    for (uint32_t i = 0; i < n; ++i) {
+        CHECK(off[i] % 16 == 0 && (i == 0 || off[i] >= off[i - 1] + len16[i - 1]), "packed layout packet %u", i);
+        want[i] = (uint16_t)(0xffffu ^ (uint32_t)oracle_compute_ones_comp(seed[i], arena + off[i], len16[i]));
+    }
+    uint8_t *d_arena;
+    uint64_t *d_blk;
+    uint16_t *d_len16, *d_seed, *d_out;
+    uint32_t *d_bad, bad = 1;
+    HIP_OK(hipMalloc((void **)&d_arena, bytes));
+    HIP_OK(hipMalloc((void **)&d_blk, ((n + 63) / 64) * sizeof *blk));
+    HIP_OK(hipMalloc((void **)&d_len16, n * sizeof *len16));
+    HIP_OK(hipMalloc((void **)&d_seed, n * sizeof *seed));
+    HIP_OK(hipMalloc((void **)&d_out, n * sizeof *got));
+    HIP_OK(hipMalloc((void **)&d_bad, sizeof *d_bad));
+    HIP_OK(hipMemcpy(d_arena, arena, bytes, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_blk, blk, ((n + 63) / 64) * sizeof *blk, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_len16, len16, n * sizeof *len16, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_seed, seed, n * sizeof *seed, hipMemcpyHostToDevice));
+    HIP_OK(hipMemset(d_bad, 0, sizeof *d_bad));
+    const uint32_t hints[3] = {64u, 340u, 1500u};  /* tiny-packet rounds kernel, mixed, mixed nt */
+    for (int h = 0; h < 3; ++h) {
+        HIP_OK(hipMemset(d_out, 0, n * sizeof *got));
+        CHECK(rns_csum_batch_packed_dev(d_arena, bytes, d_blk, d_len16, 4, d_seed, d_out, n, RNS_FLAG_COMPLEMENT,
+                                        hints[h], d_bad, st) == RNS_OK,
+              "rns_csum_batch_packed_dev hint %u", hints[h]);
+        HIP_OK(hipStreamSynchronize(st));
+        HIP_OK(hipMemcpy(got, d_out, n * sizeof *got, hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < n; ++i)
+            CHECK(got[i] == want[i], "packed batch (hint %u) packet %u (len %u): %04x != %04x", hints[h], i, len16[i],
+                  got[i], want[i]);
+    }
+    /* a cut-short arena: the packets past it are rejected (0) and counted */
+    const uint64_t cut = off[n - 5];
+    HIP_OK(hipMemset(d_out, 0xff, n * sizeof *got));
+    CHECK(rns_csum_batch_packed_dev(d_arena, cut, d_blk, d_len16, 4, d_seed, d_out, n, RNS_FLAG_COMPLEMENT, 340u,
+                                    d_bad, st) == RNS_OK, "packed, short arena");
+    HIP_OK(hipStreamSynchronize(st));
+    HIP_OK(hipMemcpy(got, d_out, n * sizeof *got, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(&bad, d_bad, sizeof bad, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n; ++i)
+        CHECK(got[i] == (i < n - 5 ? want[i] : 0u), "short arena packet %u: %04x", i, got[i]);
+    CHECK(bad == 5, "short arena: d_bad = %u (want 5)", bad);
+    hipFree(d_arena); hipFree(d_blk); hipFree(d_len16); hipFree(d_seed); hipFree(d_out); hipFree(d_bad);
+    free(len16); free(seed); free(want); free(got); free(off); free(blk); free(len32); free(arena);
+    return 0;
+}
+
+/* rns_csum_chain_dev (util.rs:112-119 over NetBuffer fragments, buf.rs:466-487): packets of
+ * 0..6 fragments of 1..700 bytes at scattered offsets, odd non-final fragments included,
+ * with and without the runs hint; half the packets' fragments are adjacent views. */
+static int test_chains(hipStream_t st)
+{
+    const uint32_t npk = 5000;
+    uint32_t *first = malloc((npk + 1) * sizeof *first);
+    uint64_t *foff = malloc(npk * 6 * sizeof *foff);
+    uint32_t *flen = malloc(npk * 6 * sizeof *flen);
+    uint16_t *seed = malloc(npk * sizeof *seed), *want = malloc(npk * sizeof *want), *got = malloc(npk * sizeof *got);
+    uint64_t pos = 0;
+    uint32_t nf = 0;
+    for (uint32_t i = 0; i < npk; ++i) {
+        const uint64_t r = next_u64();
+        const uint32_t k = (uint32_t)(r % 7);
+        const int adjacent = (r >> 8) & 1;
+        first[i] = nf;
+        seed[i] = (uint16_t)(r >> 16);
+        for (uint32_t j = 0; j < k; ++j) {
+            const uint64_t q = next_u64();
+            if (!adjacent)
+                pos += q % 29;                               /* scattered: any alignment */
+            flen[nf] = 1u + (uint32_t)((q >> 8) % 700u);
+            if (adjacent && j + 1 < k)
+                flen[nf] &= ~1u, flen[nf] += flen[nf] ? 0u : 2u;  /* even non-final fragments form a run */
+            foff[nf] = pos;
+            pos += flen[nf];
+            ++nf;
+        }
+    }
+    first[npk] = nf;
+    const uint64_t bytes = pos + 32;
+    uint8_t *arena = malloc(bytes);
+    fill_random(arena, bytes);
+    oracle_chain_batch(arena, foff, flen, first, seed, want, npk, 1);
+    uint8_t *d_arena;
+    uint64_t *d_foff;
+    uint32_t *d_flen, *d_first, *d_bad, bad = 1;
+    uint16_t *d_seed, *d_out;
+    HIP_OK(hipMalloc((void **)&d_arena, bytes));
+    HIP_OK(hipMalloc((void **)&d_foff, nf * sizeof *foff));
+    HIP_OK(hipMalloc((void **)&d_flen, nf * sizeof *flen));
+    HIP_OK(hipMalloc((void **)&d_first, (npk + 1) * sizeof *first));
+    HIP_OK(hipMalloc((void **)&d_seed, npk * sizeof *seed));
+    HIP_OK(hipMalloc((void **)&d_out, npk * sizeof *got));
+    HIP_OK(hipMalloc((void **)&d_bad, sizeof *d_bad));
+    HIP_OK(hipMemcpy(d_arena, arena, bytes, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_foff, foff, nf * sizeof *foff, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_flen, flen, nf * sizeof *flen, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_first, first, (npk + 1) * sizeof *first, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_seed, seed, npk * sizeof *seed, hipMemcpyHostToDevice));
+    HIP_OK(hipMemset(d_bad, 0, sizeof *d_bad));
+    const uint32_t flags[2] = {RNS_FLAG_COMPLEMENT, RNS_FLAG_COMPLEMENT | RNS_FLAG_CHAIN_RUNS};
+    for (int f = 0; f < 2; ++f) {
+        HIP_OK(hipMemset(d_out, 0, npk * sizeof *got));
+        CHECK(rns_csum_chain_dev(d_arena, bytes, d_foff, d_flen, nf, d_first, d_seed, d_out, npk, flags[f], 350u, NULL,
+                                 d_bad, st) == RNS_OK,
+              "rns_csum_chain_dev flags %u", flags[f]);
+        HIP_OK(hipStreamSynchronize(st));
+        HIP_OK(hipMemcpy(got, d_out, npk * sizeof *got, hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < npk; ++i)
+            CHECK(got[i] == want[i], "chain (flags %u) packet %u (%u fragments): %04x != %04x", flags[f], i,
+                  first[i + 1] - first[i], got[i], want[i]);
+    }
+    HIP_OK(hipMemcpy(&bad, d_bad, sizeof bad, hipMemcpyDeviceToHost));
+    CHECK(bad == 0, "chains: d_bad = %u", bad);
+    hipFree(d_arena); hipFree(d_foff); hipFree(d_flen); hipFree(d_first); hipFree(d_seed); hipFree(d_out);
+    hipFree(d_bad);
+    free(first); free(foff); free(flen); free(seed); free(want); free(got); free(arena);
+    return 0;
+}
+
+/* rns_tx_fill_dev then rns_rx_verify_dev on IPv4 TCP / UDP / ICMP datagrams with garbage in
+ * the checksum fields: every field must hold what the transmit call sites store (ip.rs:158-159,
+ * tcp.rs:957-973, udp.rs:158-171, icmp.rs:91-94: the oracle's util.rs functions over the
+ * datagram with the field zeroed), every other byte unchanged; the receiver (local address =
+ * the destination) accepts them all; a flipped payload byte (TCP / ICMP) or header byte is
+ * rejected as ip.rs:76-80 / tcp.rs:544-547 / icmp.rs:46-50 drop it. */
+static int test_tx_rx(hipStream_t st)
+{
+    const uint32_t n = 3000;
+    const uint8_t src[4] = {10, 0, 0, 1}, dst[4] = {10, 0, 0, 2}, dst6[16] = {0xfd, [15] = 2};
+    uint64_t *off = malloc(n * sizeof *off);
+    uint32_t *len = malloc(n * sizeof *len);
+    uint8_t *proto = malloc(n), *status = malloc(n), *want_st = malloc(n);
+    uint64_t pos = 5;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t r = next_u64();
+        pos += r % 13;
+        len[i] = 40u + (uint32_t)((r >> 8) % 1461u);
+        off[i] = pos;
+        pos += len[i];
+        proto[i] = (i % 3 == 0) ? 6 : (i % 3 == 1) ? 17 : 1;
+    }
+    const uint64_t bytes = pos + 16;
+    uint8_t *arena = malloc(bytes), *ref = malloc(bytes), *back = malloc(bytes);
+    fill_random(arena, bytes);
+    for (uint32_t i = 0; i < n; ++i) {
+        uint8_t *h = arena + off[i];
+        h[0] = 0x45; h[1] = 0; h[2] = (uint8_t)(len[i] >> 8); h[3] = (uint8_t)len[i];
+        h[6] = 0x40; h[7] = 0; h[8] = 64; h[9] = proto[i];
+        memcpy(h + 12, src, 4);
+        memcpy(h + 16, dst, 4);                      /* header checksum and L4 field keep their garbage */
+    }
+    /* expected bytes: the fields zeroed, then filled as the reference's output paths fill them */
+    memcpy(ref, arena, bytes);
+    for (uint32_t i = 0; i < n; ++i) {
+        uint8_t *h = ref + off[i], *seg = h + 20;
+        const uint32_t seglen = len[i] - 20, field = proto[i] == 6 ? 16u : proto[i] == 17 ? 6u : 2u;
+        h[10] = h[11] = 0;
+        const uint32_t ipc = (uint32_t)oracle_compute_checksum(h, 20);
+        h[10] = (uint8_t)(ipc >> 8); h[11] = (uint8_t)ipc;
+        seg[field] = seg[field + 1] = 0;
+        const int32_t ph = proto[i] == 1 ? 0 : oracle_compute_pseudo_header_checksum(src, 4, dst, 4, seglen, proto[i]);
+        const uint32_t l4 = 0xffffu ^ (uint32_t)oracle_compute_ones_comp((uint16_t)ph, seg, seglen);
+        seg[field] = (uint8_t)(l4 >> 8); seg[field + 1] = (uint8_t)l4;
+        want_st[i] = RNS_TX_IP_FILLED | RNS_TX_L4_FILLED;
+    }
+    uint8_t *d_arena, *d_status;
+    uint64_t *d_off;
+    uint32_t *d_len;
+    uint16_t *d_l4;
+    HIP_OK(hipMalloc((void **)&d_arena, bytes));
+    HIP_OK(hipMalloc((void **)&d_off, n * sizeof *off));
+    HIP_OK(hipMalloc((void **)&d_len, n * sizeof *len));
+    HIP_OK(hipMalloc((void **)&d_status, n));
+    HIP_OK(hipMalloc((void **)&d_l4, n * sizeof *d_l4));
+    HIP_OK(hipMemcpy(d_arena, arena, bytes, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_off, off, n * sizeof *off, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_len, len, n * sizeof *len, hipMemcpyHostToDevice));
+    CHECK(rns_tx_fill_dev(d_arena, bytes, d_off, d_len, n, d_status, st) == RNS_OK, "rns_tx_fill_dev");
+    HIP_OK(hipStreamSynchronize(st));
+    HIP_OK(hipMemcpy(back, d_arena, bytes, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(status, d_status, n, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n; ++i)
+        CHECK(status[i] == want_st[i], "tx status %u: %02x != %02x", i, status[i], want_st[i]);
+    uint64_t diff = 0;
+    for (uint64_t b = 0; b < bytes; ++b)
+        diff += back[b] != ref[b];
+    CHECK(diff == 0, "tx fill: %llu arena bytes differ from the oracle's", (unsigned long long)diff);
+
+    /* receive side: corrupt a payload byte of every 7th datagram, the TTL of every 11th */
+    for (uint32_t i = 0; i < n; ++i) {
+        const int payload = i % 7 == 3, header = i % 11 == 5;
+        if (payload)
+            back[off[i] + 20 + (len[i] - 20) / 2] ^= 0x5A;
+        if (header)
+            back[off[i] + 8] ^= 0x01;
+        uint8_t s_ = 0;
+        if (!header)
+            s_ |= RNS_RX_IP_OK;
+        if (proto[i] == 17)
+            s_ |= RNS_RX_L4_UNCHECKED;               /* udp.rs:126-148 never verifies */
+        else if (!payload)
+            s_ |= RNS_RX_L4_OK;
+        if ((s_ & RNS_RX_IP_OK) && (s_ & (RNS_RX_L4_OK | RNS_RX_L4_UNCHECKED)))
+            s_ |= RNS_RX_ACCEPT;
+        want_st[i] = s_;
+    }
+    HIP_OK(hipMemcpy(d_arena, back, bytes, hipMemcpyHostToDevice));
+    CHECK(rns_rx_verify_dev(d_arena, bytes, d_off, d_len, n, dst, dst6, d_status, d_l4, st) == RNS_OK,
+          "rns_rx_verify_dev");
+    HIP_OK(hipStreamSynchronize(st));
+    HIP_OK(hipMemcpy(status, d_status, n, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n; ++i)
+        CHECK(status[i] == want_st[i], "rx status %u (proto %u): %02x != %02x", i, proto[i], status[i], want_st[i]);
+    hipFree(d_arena); hipFree(d_off); hipFree(d_len); hipFree(d_status); hipFree(d_l4);
+    free(off); free(len); free(proto); free(status); free(want_st); free(arena); free(ref); free(back);
+    return 0;
+}
 
 int main(void)
 {
@@ -143,6 +394,11 @@ int main(void)
     uint32_t bad = 1;
     HIP_OK(hipMemcpy(&bad, d_bad, sizeof bad, hipMemcpyDeviceToHost));
     CHECK(bad == 0, "d_bad = %u", bad);
+
+    /* 2b. the packed entry bench.py times, the fragment-chain entry, transmit finalize and
+     *     receive verify: each against the oracle's util.rs restatement */
+    if (test_packed(st) || test_chains(st) || test_tx_rx(st))
+        return 2;
 
     /* 3. errors come back as status codes, never as aborts */
     CHECK(rns_csum_batch_dev(NULL, bytes, d_off, d_len, d_seed, d_out, n, 0, 0, NULL, st) == RNS_E_INVALID,

@@ -34,7 +34,7 @@ class _Batch:
 class CpuEngine(bench.GpuEngine):
     """Stand-in for bench.GpuEngine: same interface, oracle compute on CPU tensors."""
     def __init__(self, config, rank, local_rank, shape=None, steps=0, world=1, strong=False, compact="64",
-                 op="csum"):
+                 op="csum", min_batches=1, shard=None):
         assert op == "csum"
         self.torch = torch
         self.device = torch.device("cpu")
@@ -162,7 +162,7 @@ class CpuVerifyEngine(bench.GpuEngine):
     the host (headers from workloads, checksums by the oracle's transmit restatement,
     the same corruptions), each step = the oracle's receive restatement per datagram."""
     def __init__(self, config, rank, local_rank, shape=None, steps=0, world=1, strong=False, compact="64",
-                 op="csum"):
+                 op="csum", min_batches=1, shard=None):
         assert op == "verify"
         self.torch, self.op = torch, op
         self.device = torch.device("cpu")
