@@ -485,6 +485,9 @@ class GpuEngine:
         from rustnetworkstack_amd import _lib
         if self.op == "verify":
             return "csum_mixed_kernel<RX> (rns_rx_verify_dev: class-sorted data pass + header stash)"
+        if self.packed and self.layout.n and int(self.layout.off[0]) % 16 == 0:
+            return ("csum_stream_kernel (packed form, 16-byte-aligned packets: one wave streams each 64-packet "
+                    "block as 1 KiB rows, prefix sums per packet)")
         return _lib.load().rns_csum_shape_name(int(round(self.layout.mean_len))).decode()
 
     def out_sample(self, count: int):

@@ -203,6 +203,18 @@ int rns_rx_verify_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64
                       uint32_t n, const uint8_t *local_ipv4, const uint8_t *local_ipv6, uint8_t *d_status,
                       uint16_t *d_l4_sum, void *stream);
 
+/* Receive verify of a PACKED receive arena (the descriptor form of
+ * rns_csum_batch_packed_dev: u16 lengths, d_blk_off[b] = offset of datagram 64*b),
+ * with datagrams starting on 16-byte boundaries (align_log2 >= 4; 2048-byte receive
+ * slots qualify): per datagram exactly the checks and status bits of rns_rx_verify_dev
+ * (ip.rs:65-131, tcp.rs:838-850, icmp.rs:44-75).  One wave streams each 64-datagram
+ * block's bytes as whole 1 KiB rows whatever the datagram sizes (the stream kernel),
+ * which keeps ACK-sized datagrams at the plain checksum's rate.  align_log2 < 4 is
+ * RNS_E_INVALID. */
+int rns_rx_verify_packed_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_blk_off,
+                             const uint16_t *d_len16, uint32_t align_log2, uint32_t n, const uint8_t *local_ipv4,
+                             const uint8_t *local_ipv6, uint8_t *d_status, uint16_t *d_l4_sum, void *stream);
+
 /* Transmit finalize (SURVEY a6, §8f row 2 for whole datagrams): for each finished
  * outgoing IP datagram d_arena[d_off[i] .. + d_len[i]), the checksums the stack's
  * transmit path stores — tcp_output (tcp.rs:957-973: pseudo-header from the header's

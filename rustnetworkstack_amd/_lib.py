@@ -52,6 +52,7 @@ EXPORTED_SYMBOLS = (
     "rns_csum_chain_dev",
     "rns_csum_fill_dev",
     "rns_rx_verify_dev",
+    "rns_rx_verify_packed_dev",
     "rns_tx_fill_dev",
     "rns_host_ctx_create",
     "rns_host_ctx_destroy",
@@ -122,6 +123,7 @@ _SIGNATURES = {
     "rns_csum_chain_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp]),
     "rns_csum_fill_dev": (_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u32, _vp, _u32, _u32, _vp, _vp]),
     "rns_rx_verify_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),
+    "rns_rx_verify_packed_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp]),
     "rns_tx_fill_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp]),
     "rns_host_ctx_create": (_int, [_int, _u64, _u32, ctypes.POINTER(_vp)]),
     "rns_host_ctx_destroy": (_int, [_vp]),

@@ -359,6 +359,36 @@ def rx_verify(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, loca
     return status
 
 
+def rx_verify_packed(arena: torch.Tensor, blk_off: torch.Tensor, len16: torch.Tensor, local_ipv4: bytes,
+                     local_ipv6: bytes, *, align_log2: int = 4, status: torch.Tensor | None = None,
+                     l4_sum: torch.Tensor | None = None) -> torch.Tensor:
+    """Receive verify of a PACKED arena of datagrams (rns_rx_verify_packed_dev: u16 lengths,
+    one offset per 64 datagrams, 16-byte-aligned starts): the same uint8 status per datagram
+    as rx_verify."""
+    _require_cuda(arena, "arena", (torch.uint8,))
+    _require_cuda(blk_off, "blk_off", (torch.int64,))
+    _require_cuda(len16, "len16", _U16)
+    if len(local_ipv4) != 4 or len(local_ipv6) != 16:
+        raise ValueError("local_ipv4 must be 4 bytes and local_ipv6 16 bytes")
+    n = len16.numel()
+    if blk_off.numel() < (n + 63) // 64:
+        raise ValueError("blk_off needs one offset per 64 datagrams")
+    dev = arena.device
+    lib = _lib.load()
+    if status is None:
+        status = torch.empty(n, dtype=torch.uint8, device=dev)
+    l4_ptr = None
+    if l4_sum is not None:
+        _require_cuda(l4_sum, "l4_sum", _U16)
+        l4_ptr = l4_sum.data_ptr()
+    with torch.cuda.device(dev):
+        st = lib.rns_rx_verify_packed_dev(arena.data_ptr(), arena.numel(), blk_off.data_ptr(), len16.data_ptr(),
+                                          int(align_log2), n, bytes(local_ipv4), bytes(local_ipv6),
+                                          status.data_ptr(), l4_ptr, _stream_handle(dev))
+    _lib.check(st, "rns_rx_verify_packed_dev")
+    return status
+
+
 def tx_fill(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, *,
             status: torch.Tensor | None = None) -> torch.Tensor:
     """Transmit finalize of a batch of outgoing IP datagrams (rns_tx_fill_dev): the

@@ -1288,6 +1288,65 @@ __device__ __forceinline__ uint8_t rx_verdict(uint32_t m, uint32_t hdr_res, uint
     return static_cast<uint8_t>(st);
 }
 
+// Receive verify, owner-lane finish for one datagram: mine = the whole datagram's word
+// sum T (LE for <= 128 KiB, exact BE mod 2^32 above), own = its stashed chunks 0..NS-1
+// from the 16-byte-aligned chunk holding its first byte (bytes outside the datagram read
+// as zero; a chunk past NS reads as zero), s = start & 15.  Header H from the stash (seed
+// 0, <= 60 bytes); L4 = T - H, seeded with the pseudo-header sum.  Both parts start at
+// the datagram's parity (the header length is even).  Returns the RNS_RX_* status;
+// l4_res = the complemented L4 sum.
+template <int NS>
+__device__ __forceinline__ uint8_t rx_finish(const CsumArgs &a, const uint4 *own, uint32_t mine, uint32_t s,
+                                             uint32_t d_len, bool odd, bool big, bool present, uint32_t &l4_res)
+{
+    uint4 ch[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        ch[i] = own[i];
+    uint32_t head[6];
+    if (kRxAlignedFast && s == 0) {  // 16-byte-aligned datagram: the dwords as they are
+        const uint32_t w6[6] = {ch[0].x, ch[0].y, ch[0].z, ch[0].w, ch[1].x, ch[1].y};
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            head[k] = w6[k];
+    } else {
+        head_from_stash(ch, s, head);
+    }
+    const RxParse rp = present ? rx_parse(head, d_len, a.local4_sum, a.local6_sum) : RxParse{kMetaMalformed, 0u, 0u};
+    uint32_t hdr_res = 0;
+    l4_res = 0;
+    if (!(rp.meta & kMetaMalformed)) {
+        const int hlo = static_cast<int>(s), hhi = hlo + static_cast<int>(rp.hdr);  // <= 15 + 60
+        uint32_t H;
+        if (kRxAlignedFast && hlo == 0 && hhi == 20) {  // aligned IPv4 header, no options: 5 dwords
+            H = __builtin_amdgcn_sad_u16(ch[0].x, 0, 0u);
+            H = __builtin_amdgcn_sad_u16(ch[0].y, 0, H);
+            H = __builtin_amdgcn_sad_u16(ch[0].z, 0, H);
+            H = __builtin_amdgcn_sad_u16(ch[0].w, 0, H);
+            H = __builtin_amdgcn_sad_u16(ch[1].x, 0, H);
+        } else {
+            H = stash_sum_le(ch, hlo, hhi);
+        }
+        uint4 tail[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+        if (hhi > 48) {  // IPv6 past offset 8, IPv4 with options: header bytes in chunks 3-4
+            tail[0] = own[3];
+            if constexpr (NS > 4)
+                tail[1] = own[4];
+            H += stash_sum_le(tail, hlo - 48, hhi - 48);
+        }
+        hdr_res = finalize_bits(H, odd, false, 0u, true, RNS_FLAG_COMPLEMENT);
+        if (rp.meta & kMetaL4Checked) {
+            uint32_t l4 = mine - H;
+            if (big) {  // > 128 KiB (rare): the exact big-endian sums, mod 2^32
+                const uint4 all[5] = {ch[0], ch[1], ch[2], tail[0], tail[1]};
+                l4 = mine - stash_sum_be(all, hlo, hhi, odd);
+            }
+            l4_res = finalize_bits(l4, odd, big, rp.ph, true, RNS_FLAG_COMPLEMENT);
+        }
+    }
+    return rx_verdict(rp.meta, hdr_res, l4_res);
+}
+
 // One packet's descriptor.  Loads are branch-free (an index past the batch re-reads
 // its last packet and the result is discarded), so no wait is forced at a branch merge.
 // With a buffer descriptor (arena < 4 GiB) the offset is held in 32 bits: one past
@@ -1535,58 +1594,13 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX
             continue;
         }
         if constexpr (RX) {
-            // mine = the whole datagram's word sum T.  Header H from the stash (seed 0,
-            // <= 60 bytes); L4 = T - H, seeded with the pseudo-header sum.  Both parts
-            // start at the datagram's parity (the header length is even).
-            uint4 ch[3];
+            // mine = the whole datagram's word sum T (see rx_finish)
             wave_lds_fence();  // the stash was written by other lanes of this wave
-            const uint4 *mine_st = st + pos * kNS;
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-                ch[i] = mine_st[i];
-            const uint32_t s = static_cast<uint32_t>(d_start & 15);
-            uint32_t head[6];
-            if (kRxAlignedFast && s == 0) {  // 16-byte-aligned datagram: the dwords as they are
-                const uint32_t w6[6] = {ch[0].x, ch[0].y, ch[0].z, ch[0].w, ch[1].x, ch[1].y};
-#pragma unroll
-                for (int k = 0; k < 6; ++k)
-                    head[k] = w6[k];
-            } else {
-                head_from_stash(ch, s, head);
-            }
-            const RxParse rp = (live && d_len != 0) ? rx_parse(head, d_len, a.local4_sum, a.local6_sum)
-                                                    : RxParse{kMetaMalformed, 0u, 0u};
-            uint32_t hdr_res = 0, l4_res = 0;
-            if (!(rp.meta & kMetaMalformed)) {
-                const int hlo = static_cast<int>(s), hhi = hlo + static_cast<int>(rp.hdr);  // <= 15 + 60
-                uint32_t H;
-                if (kRxAlignedFast && hlo == 0 && hhi == 20) {  // aligned IPv4 header, no options: 5 dwords
-                    H = __builtin_amdgcn_sad_u16(ch[0].x, 0, 0u);
-                    H = __builtin_amdgcn_sad_u16(ch[0].y, 0, H);
-                    H = __builtin_amdgcn_sad_u16(ch[0].z, 0, H);
-                    H = __builtin_amdgcn_sad_u16(ch[0].w, 0, H);
-                    H = __builtin_amdgcn_sad_u16(ch[1].x, 0, H);
-                } else {
-                    H = stash_sum_le(ch, hlo, hhi);
-                }
-                uint4 tail[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-                if (hhi > 48) {  // IPv6 past offset 8, IPv4 with options: header bytes in chunks 3-4
-                    tail[0] = mine_st[3];
-                    tail[1] = mine_st[4];
-                    H += stash_sum_le(tail, hlo - 48, hhi - 48);
-                }
-                hdr_res = finalize_bits(H, odd, false, 0u, true, RNS_FLAG_COMPLEMENT);
-                if (rp.meta & kMetaL4Checked) {
-                    uint32_t l4 = mine - H;
-                    if (big) {  // > 128 KiB (rare): the exact big-endian sums, mod 2^32
-                        const uint4 all[5] = {ch[0], ch[1], ch[2], tail[0], tail[1]};
-                        l4 = mine - stash_sum_be(all, hlo, hhi, odd);
-                    }
-                    l4_res = finalize_bits(l4, odd, big, rp.ph, true, RNS_FLAG_COMPLEMENT);
-                }
-            }
+            uint32_t l4_res = 0;
+            const uint8_t stv = rx_finish<kNS>(a, st + pos * kNS, mine, static_cast<uint32_t>(d_start & 15), d_len, odd,
+                                               big, live && d_len != 0, l4_res);
             if (live) {
-                a.status[p] = rx_verdict(rp.meta, hdr_res, l4_res);
+                a.status[p] = stv;
                 if (a.l4_out)
                     a.l4_out[p] = static_cast<uint16_t>(l4_res);
             }
@@ -1872,6 +1886,248 @@ __global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// v4: "stream" kernel — the packed form with 16-byte-aligned packets (align_log2 >= 4).
+//
+// A wave owns a 64-packet block.  Its packets lie back to back from blk_off[b], each
+// starting on a 16-byte boundary, so the block is one contiguous REGION of the arena
+// in which every 16-byte chunk belongs to exactly one packet (its tail chunk also
+// holds the padding up to the next boundary).  The wave streams the region as rows
+// of 64 chunks — lane l loads chunk 64k + l of row k, one fully coalesced 1 KiB load
+// per row, D rows in flight — whatever the packet sizes: no size classes, no sort, no
+// partially used loads.  Per row every lane sums its chunk's LE 16-bit words
+// (v_sad_u16), a DPP scan turns the row into prefix sums P, and the region prefix at
+// each packet's LAST chunk is kept.  A packet's word sum is the difference of the
+// prefixes at its own last chunk and at the previous non-empty packet's.  Packets
+// are at most 65535 bytes (u16 lengths), so every packet's LE sum is exact in u32 and
+// the u32 prefixes may wrap: the difference is exact.
+//
+// Per row: the owners whose packet ends in the row publish (row tag, packet, valid
+// bytes) to an LDS slot indexed by the lane that loads that chunk; every lane reads its
+// slot, zeroes the padding bytes of an end chunk, and an end lane stores its prefix to
+// pend[packet].  ~25 VALU + 3 LDS operations per KiB, one VMEM load per KiB.
+//
+// A block whose region does not start 16-byte aligned (a first packet at an unaligned
+// offset, or an unaligned arena base) takes a simple per-packet wave loop instead.
+// ---------------------------------------------------------------------------
+// Inclusive prefix sum over the 64 lanes (wave_excl_scan's DPP sequence).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+    uint32_t x = v;
+    x += dpp_or_zero<0x111>(v);              // row_shr:1
+    x += dpp_or_zero<0x112>(v);              // row_shr:2
+    x += dpp_or_zero<0x113>(v);              // row_shr:3
+    x += dpp_or_zero<0x114, 0xF, 0xE>(x);    // row_shr:4, banks 1-3
+    x += dpp_or_zero<0x118, 0xF, 0xC>(x);    // row_shr:8, banks 2-3
+    x += dpp_or_zero<0x142, 0xA, 0xF>(x);    // row_bcast:15 into rows 1 and 3
+    x += dpp_or_zero<0x143, 0xC, 0xF>(x);    // row_bcast:31 into rows 2 and 3
+    return x;
+}
+
+// Keep the first c (1..16) bytes of a chunk: the 128-bit mask (1 << 8c) - 1 as two
+// 64-bit halves (shift counts stay in 0..63).
+__device__ __forceinline__ uint4 keep_first(uint4 v, uint32_t c)
+{
+    const uint32_t bits = c * 8u;                                    // 8..128
+    const uint64_t lo = ~0ull >> (64u - min(bits, 64u));
+    const uint64_t hi = bits > 64u ? ~0ull >> ((128u - bits) & 63u) : 0ull;
+    v.x &= static_cast<uint32_t>(lo);
+    v.y &= static_cast<uint32_t>(lo >> 32);
+    v.z &= static_cast<uint32_t>(hi);
+    v.w &= static_cast<uint32_t>(hi >> 32);
+    return v;
+}
+
+#ifndef RNS_STREAM_D  // rows (1 KiB loads) in flight per wave
+#define RNS_STREAM_D 4
+#endif
+#ifndef RNS_STREAM_OCC  // waves/SIMD bound
+#define RNS_STREAM_OCC 8
+#endif
+constexpr int kStreamD = RNS_STREAM_D;
+
+// MODE kStashNone: the plain batch checksum (seed, optional complement, u16 out).
+// MODE kStashHead: receive verify (rns_rx_verify_packed_dev): the lanes that load a
+// datagram's first 4 chunks (64 bytes: every IPv4 header incl. options, the IPv6 header)
+// also copy them to an LDS stash, and the owner finishes exactly as the class kernel's
+// receive verify does (rx_finish).
+#ifndef RNS_STREAM_RX_OCC  // waves/SIMD bound of the receive-verify instantiation (its finish needs registers)
+#define RNS_STREAM_RX_OCC 6
+#endif
+template <int MODE, bool NT, bool BUF>
+__global__ __launch_bounds__(64, MODE == kStashHead ? RNS_STREAM_RX_OCC : RNS_STREAM_OCC) void csum_stream_kernel(
+    const CsumArgs a)
+{
+    static_assert(MODE == kStashNone || MODE == kStashHead, "stream modes: plain, receive verify");
+    constexpr bool RX = MODE == kStashHead;
+    constexpr int kNS = RX ? 5 : 1;  // stash chunks per datagram (the unaligned path fills 5)
+    // entry bits: [31:18] row tag, [17] head chunk, [16:15] head index, [14] end chunk,
+    // [13:8] packet, [7] first chunk, [3:0] valid bytes - 1 (end chunk)
+    constexpr uint32_t kTagShift = 18, kHead = 1u << 17, kEnd = 1u << 14, kStart = 1u << 7;
+    __shared__ uint32_t tab[64];     // per row: the entry of the chunk lane l loads
+    __shared__ uint32_t pend[64];    // per packet: the region prefix through its last chunk
+    __shared__ uint32_t pstart[64];  // per packet: the region prefix before its first chunk
+    __shared__ uint4 stash[RX ? 64 * kNS : 1];
+    const uint32_t lane = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
+    const uint64_t recs = buf_records(a);
+    const uint64_t nblk = (static_cast<uint64_t>(a.n) + 63) >> 6;
+
+    for (uint64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const uint64_t p = blk * 64 + lane;
+        const bool live = p < a.n;
+        const uint64_t q = live ? p : a.n - 1;
+        const uint32_t len = live ? static_cast<uint32_t>(a.len16[q]) : 0u;
+        const uint32_t seed = (!RX && a.seed && live) ? static_cast<uint32_t>(a.seed[q]) : 0u;
+        const uint64_t r0 = a.blk_off[blk] + a.base_adjust;               // the block's first packet
+        const uint32_t pad = (len + a.align_mask) & ~a.align_mask;        // a multiple of 16
+        const uint32_t incl = wave_incl_scan(pad);
+        const uint32_t excl = incl - pad;
+        const uint64_t start = r0 + excl;
+        const bool ok = start <= a.arena_bytes && len <= a.arena_bytes - start;
+        const bool nonempty = len != 0;
+        uint32_t mine = 0;
+        bool odd = false;
+
+        if ((r0 & 15) == 0) {
+            // ---- stream path ----
+            const uint32_t total = __builtin_amdgcn_readlane(incl, 63);   // region bytes (multiple of 16)
+            const uint32_t nrows = (total + 1023) >> 10;
+            const uint32_t c0 = excl >> 4;                                    // first chunk, region-relative
+            const uint32_t e = nonempty ? (excl + len - 1) >> 4 : 0xFFFFFFFFu;  // last chunk
+            const uint32_t ent = (lane << 8) | ((len - 1) & 15u);            // packet | valid bytes - 1
+            tab[lane] = 0xFFFFFFFFu;                                          // tag 0x3FFF: never a row
+            wave_lds_fence();
+            uint32_t carry = 0;
+            uint4 v[kStreamD];
+            auto issue = [&](uint32_t k, uint4 &dst) {  // row k: chunk 64k + lane of the region
+                const uint64_t off = r0 + (static_cast<uint64_t>(k) << 10) + (lane << 4);
+                const bool in = k < nrows && off + 16 <= recs;
+                if constexpr (BUF) {
+                    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(
+                        rsrc, in ? static_cast<uint32_t>(off) : kOobOffset, 0, NT ? kNtAux : 0);
+                    dst = make_uint4(x.x, x.y, x.z, x.w);
+                } else {
+                    const uint4 x = load_chunk<NT>(a.arena + (in ? off : 0));
+                    dst = in ? x : make_uint4(0, 0, 0, 0);
+                }
+            };
+            // (issue order pinned: the loop consumes v[0] first, so its load must be the oldest
+            // on entry as on the back edge, or the compiler waits for all of them)
+#pragma unroll
+            for (int j = 0; j < kStreamD; ++j) {
+                issue(j, v[j]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            for (uint32_t k0 = 0; k0 < nrows; k0 += kStreamD) {
+#pragma unroll
+                for (int j = 0; j < kStreamD; ++j) {
+                    const uint32_t k = k0 + j;
+                    const uint32_t tag = k << kTagShift;
+                    // owners publish at the lanes that load their chunks in row k: the end chunk
+                    // (and, receive verify, the first 4 chunks)
+                    // (and its first chunk: padding chunks between packets, align_log2 > 4, belong
+                    // to no packet, so a packet's sum is its end prefix minus its own start prefix)
+                    if constexpr (RX) {
+#pragma unroll
+                        for (uint32_t h = 0; h < 4; ++h) {
+                            const uint32_t c = c0 + h;
+                            if (nonempty && c <= e && (c >> 6) == k)
+                                tab[c & 63] = tag | kHead | (h << 15) | (h == 0 ? kStart : 0u) | (c == e ? kEnd : 0u) |
+                                              ent;
+                        }
+                        if (nonempty && e >= c0 + 4 && (e >> 6) == k)
+                            tab[e & 63] = tag | kEnd | ent;
+                    } else {
+                        if (nonempty && (c0 >> 6) == k)
+                            tab[c0 & 63] = tag | kStart | (c0 == e ? kEnd : 0u) | ent;
+                        if (nonempty && e != c0 && (e >> 6) == k)
+                            tab[e & 63] = tag | kEnd | ent;
+                    }
+                    wave_lds_fence();
+                    const uint32_t t = tab[lane];
+                    const bool mark = (t >> kTagShift) == k;
+                    const bool is_end = mark && (t & kEnd);
+                    uint4 x = v[j];
+                    if (__ballot(is_end && (t & 15u) != 15u))  // a partial end chunk in this row
+                        x = keep_first(x, is_end ? (t & 15u) + 1u : 16u);
+                    if constexpr (RX) {
+                        if (mark && (t & kHead))
+                            stash[((t >> 8) & 63u) * kNS + ((t >> 15) & 3u)] = x;
+                    }
+                    uint32_t s = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
+                    s = __builtin_amdgcn_sad_u16(x.y, 0, s);
+                    s = __builtin_amdgcn_sad_u16(x.z, 0, s);
+                    s = __builtin_amdgcn_sad_u16(x.w, 0, s);
+                    // the row D ahead into the registers this row just freed (past the region: no
+                    // memory traffic).  Issued only after the row is consumed, so the loop-carried
+                    // registers need no copy — a copy at the back edge waits for every load in flight.
+                    __builtin_amdgcn_sched_barrier(0);
+                    issue(k + kStreamD, v[j]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const uint32_t inc = wave_incl_scan(s);
+                    if (mark && (t & kStart))
+                        pstart[(t >> 8) & 63u] = carry + inc - s;
+                    if (is_end)
+                        pend[(t >> 8) & 63u] = carry + inc;
+                    carry += __builtin_amdgcn_readlane(inc, 63);
+                    wave_lds_fence();
+                }
+            }
+            // a packet's sum: the region prefix through its last chunk minus the prefix before its
+            // first (u32 differences: exact, a packet's LE sum is < 2^32)
+            mine = nonempty ? pend[lane] - pstart[lane] : 0u;
+        } else {
+            // ---- unaligned region (rare): the whole wave sums one packet at a time ----
+            uint64_t todo = __ballot(nonempty && ok);
+            while (todo) {
+                const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
+                todo &= todo - 1;
+                const uint64_t st = (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start >> 32), o))
+                                     << 32) | __builtin_amdgcn_readlane(static_cast<uint32_t>(start), o);
+                const uint32_t L = __builtin_amdgcn_readlane(len, o);
+                const Pkt k = make_pkt(st, L);
+                uint32_t acc = 0;
+                for (uint32_t cc = 0; cc < k.nch; cc += 64) {
+                    uint4 w[1];
+                    issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, w);
+                    mask_edges<64, 1, 1>(k, cc + lane, w);
+                    if constexpr (RX) {
+                        if (cc == 0 && lane < static_cast<uint32_t>(kNS))
+                            stash[o * kNS + lane] = lane < k.nch ? w[0] : make_uint4(0, 0, 0, 0);
+                    }
+                    acc = sum_le<1, 1>(w, acc);
+                }
+                const uint32_t sum = group_allreduce<64>(acc);
+                mine = lane == o ? sum : mine;
+            }
+            odd = start & 1;
+        }
+        wave_lds_fence();
+        if constexpr (RX) {
+            uint32_t l4_res = 0;
+            const uint8_t stv = rx_finish<kNS>(a, stash + lane * kNS, mine, static_cast<uint32_t>(start & 15), len, odd,
+                                               false, live && ok && nonempty, l4_res);
+            if (live) {
+                a.status[p] = stv;
+                if (a.l4_out)
+                    a.l4_out[p] = static_cast<uint16_t>(l4_res);
+            }
+        } else {
+            const uint16_t res = finalize_bits(mine, odd, false, seed, ok, a.flags);
+            if (live)
+                a.out[p] = res;  // 64 consecutive u16: one 128-byte store
+            if (a.bad) {
+                const uint64_t rejected = __ballot(live && !ok);
+                if (rejected && lane == 0)
+                    atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
+            }
+        }
+        wave_lds_fence();  // the next block rewrites tab / pend / stash
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void splitmix64_fill_kernel(uint8_t *buf, uint64_t nbytes, uint64_t seed)
 {
     const uint64_t nwords = (nbytes + 7) / 8;
@@ -2034,9 +2290,24 @@ Shape pick_shape(uint32_t len_hint)
 // The packed form's kernels (separate instantiations, so the explicit-descriptor
 // kernels carry no packed-form code): the mixed kernel, or for tiny packets the
 // rounds kernel with pick_shape's G=4, U=1 shape.
+#ifndef RNS_STREAM  // A/B knob: 0 = the packed form always runs the class / rounds kernels
+#define RNS_STREAM 1
+#endif
+#ifndef RNS_STREAM_NT  // nontemporal loads in the stream kernel
+#define RNS_STREAM_NT 1
+#endif
 int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
 {
     const bool nt = (sh.variant & 2u) != 0, buf = buf_records(a) < kOobOffset;
+    if (RNS_STREAM && a.align_mask >= 15u) {  // 16-byte-aligned packets: one wave streams each 64-packet block
+        const uint64_t blocks = (static_cast<uint64_t>(a.n) + 63) / 64;
+        const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(blocks, 0x7FFFFFFFu))), block(64);
+        if (buf)
+            hipLaunchKernelGGL((csum_stream_kernel<kStashNone, RNS_STREAM_NT != 0, true>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_stream_kernel<kStashNone, RNS_STREAM_NT != 0, false>), grid, block, 0, st, a);
+        return hip_status(hipGetLastError());
+    }
     const uint64_t batches = (static_cast<uint64_t>(a.n) + 63) / 64;  // one wave per 64 packets
     const uint64_t wpb = ((sh.variant & 4u) ? kMixedBlock<false> : kBlock) / 64;  // waves per workgroup
     uint64_t blocks = (batches + wpb - 1) / wpb;
@@ -2429,6 +2700,38 @@ int rns_rx_verify_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64
         hipLaunchKernelGGL((csum_mixed_kernel<false, kNT, true, false, true>), grid, block, 0, st, a);
     else
         hipLaunchKernelGGL((csum_mixed_kernel<false, kNT, false, false, true>), grid, block, 0, st, a);
+    return hip_status(hipGetLastError());
+}
+
+int rns_rx_verify_packed_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_blk_off,
+                             const uint16_t *d_len16, uint32_t align_log2, uint32_t n, const uint8_t *local_ipv4,
+                             const uint8_t *local_ipv6, uint8_t *d_status, uint16_t *d_l4_sum, void *stream)
+{
+    if (n == 0)
+        return RNS_OK;
+    if (!d_arena || !d_blk_off || !d_len16 || !d_status || !local_ipv4 || !local_ipv6 || align_log2 < 4 ||
+        align_log2 > 12)
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    CsumArgs a{};
+    set_arena(a, d_arena, arena_bytes);
+    a.len16 = d_len16;
+    a.blk_off = d_blk_off;
+    a.align_mask = (1u << align_log2) - 1u;
+    a.n = n;
+    a.flags = RNS_FLAG_COMPLEMENT;
+    a.status = d_status;
+    a.l4_out = d_l4_sum;
+    a.local4_sum = be_sum(local_ipv4, 4);
+    a.local6_sum = be_sum(local_ipv6, 16);
+    const uint64_t blocks = (static_cast<uint64_t>(n) + 63) / 64;
+    const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(blocks, 0x7FFFFFFFu))), block(64);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (buf_records(a) < kOobOffset)
+        hipLaunchKernelGGL((csum_stream_kernel<kStashHead, RNS_STREAM_NT != 0, true>), grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL((csum_stream_kernel<kStashHead, RNS_STREAM_NT != 0, false>), grid, block, 0, st, a);
     return hip_status(hipGetLastError());
 }
 

@@ -113,14 +113,64 @@ def test_packed_layout_rejects_long_lengths():
 
 
 @pytest.mark.parametrize("name", ["c2_64B", "c3_1500B", "c4_9000B", "c5_imix"])
-def test_full_size_packed_equals_64bit(name):
-    """Every packet of each BASELINE.json config (the synthetic layouts are packed at
-    16 bytes): packed == 64-bit descriptors, which test_gpu_parity checks packet by
-    packet against the oracle."""
+def test_full_size_packed_bit_exact(oracle, name):
+    """Every packet of each BASELINE.json config through the packed entry bench.py times
+    (the synthetic layouts are packed at 16 bytes: the stream kernel), against the C
+    oracle, and equal to the 64-bit descriptor path."""
     lay = make_layout(name)
     b = DeviceBatch(lay, DEV)
+    got = b.launcher(complement=True, packed=True)().clone()
     ref = csum_batch(b.arena, b.off, b.length, b.seed, complement=True, len_hint=int(lay.mean_len))
-    got = b.launcher(complement=True, packed=True)()
     assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+    expect = oracle.batch(b.host_arena(), lay.off, lay.length, lay.seed, complement=True, threads=16)
+    assert np.array_equal(host_u16(got), expect)
     del b
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("first_off,base_shift", [(5, 0), (0, 3), (16, 7), (1, 15)])
+def test_unaligned_regions(oracle, first_off, base_shift):
+    """align_log2 >= 4 but the blocks' regions do not start 16-byte aligned in memory:
+    a first packet at an unaligned offset (every packet of the batch then shares its
+    misalignment) or an arena base that is not 16-byte aligned.  Every packet against
+    the C oracle (the stream kernel's per-packet path for such blocks)."""
+    rng = np.random.default_rng(first_off * 31 + base_shift)
+    n = 3 * 64 + 17
+    ln = rng.integers(0, 2000, n).astype(np.uint32)
+    ln[::9] = 0
+    sd = rng.integers(0, 1 << 16, n).astype(np.uint16)
+    blk, poff, end = packed_layout(ln, 4, first_off)
+    arena = O.splitmix64_bytes(0x51 + first_off, end + 16)
+    expect = oracle.batch(arena, poff, ln, sd, complement=True)
+    big = torch.zeros(end + 16 + base_shift, dtype=torch.uint8, device=DEV)
+    big[base_shift:].copy_(torch.from_numpy(arena))
+    view = big[base_shift:]  # data_ptr() = base + base_shift
+    for hint in (64, 340, 1500):
+        got = host_u16(csum_batch_packed(view, dev(blk.astype(np.uint64), np.int64), dev(ln.astype(np.uint16), np.int16),
+                                         dev(sd, np.int16), align_log2=4, complement=True, len_hint=hint))
+        assert np.array_equal(got, expect), hint
+
+
+@pytest.mark.parametrize("pattern", ["zero", "ff", "random"])
+def test_stream_rows_many_ends_and_empties(oracle, pattern):
+    """Blocks whose packets end on every chunk of a row (16-byte packets), empty packets
+    between them, packets spanning many rows (up to 65535 B), all-zero and all-0xff
+    payloads (the end-around fold's zero cases), with and without seeds."""
+    rng = np.random.default_rng({"zero": 1, "ff": 2, "random": 3}[pattern])
+    n = 64 * 40 + 3
+    kind = rng.integers(0, 4, n)
+    ln = np.select([kind == 0, kind == 1, kind == 2], [0, rng.integers(1, 17, n), rng.integers(17, 600, n)],
+                   rng.integers(600, 65536, n)).astype(np.uint32)
+    ln[:64] = 16                                # a block of 64 one-chunk packets: 64 ends in one row
+    ln[64:128] = np.arange(1, 65)               # ends at every valid-byte count
+    blk, poff, end = packed_layout(ln, 4, 32)
+    if pattern == "zero":
+        arena = np.zeros(end + 16, dtype=np.uint8)
+    elif pattern == "ff":
+        arena = np.full(end + 16, 0xFF, dtype=np.uint8)
+    else:
+        arena = O.splitmix64_bytes(99, end + 16)
+    for sd in (None, rng.integers(0, 1 << 16, n).astype(np.uint16), np.zeros(n, dtype=np.uint16)):
+        expect = oracle.batch(arena, poff, ln, sd, complement=False)
+        got = run_packed(arena, blk, ln, sd, 4, len_hint=340)
+        assert np.array_equal(got, expect)

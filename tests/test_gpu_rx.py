@@ -184,3 +184,71 @@ def test_tiny_datagrams_capped_grid_every_status():
     want = np.full(n, _lib.RNS_RX_ACCEPT | _lib.RNS_RX_IP_OK | _lib.RNS_RX_L4_OK, dtype=np.uint8)
     want[corrupt_mask(n)] = _lib.RNS_RX_IP_OK
     assert np.array_equal(st, want)
+
+
+# --- packed receive arenas (rns_rx_verify_packed_dev: the stream kernel) ---------------
+def run_packed_rx(pkts, align_log2, first_off, base_shift=0):
+    from rustnetworkstack_amd.batch import packed_layout, rx_verify_packed
+    ln = np.array([len(p) for p in pkts], dtype=np.uint32)
+    blk, poff, end = packed_layout(ln, align_log2, first_off)
+    arena = np.full(end + 16 + base_shift, 0xA5, dtype=np.uint8)   # padding never counts
+    for o, p in zip(poff.tolist(), pkts):
+        arena[base_shift + o:base_shift + o + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    big = torch.from_numpy(arena).to(DEV)
+    l4 = torch.empty(len(pkts), dtype=torch.uint16, device=DEV)
+    st = rx_verify_packed(big[base_shift:], dev(blk.astype(np.uint64), np.int64), dev(ln.astype(np.uint16), np.int16),
+                          L4, L6, align_log2=align_log2, l4_sum=l4)
+    return st.cpu().numpy(), l4.view(torch.int16).cpu().numpy().view(np.uint16)
+
+
+@pytest.mark.parametrize("align_log2,first_off,base_shift", [(4, 0, 0), (4, 32, 0), (11, 0, 0), (4, 5, 0), (4, 0, 3)])
+def test_packed_mixed_datagrams_match_reference_path(oracle, align_log2, first_off, base_shift):
+    """Every kind of datagram (valid, corrupted, fragments, options, UDP, ICMP, garbage)
+    packed at 16 bytes and in 2048-byte slots; an unaligned first offset and an unaligned
+    arena base take the kernel's per-datagram path.  Status and L4 sum per datagram
+    against the reference's receive path."""
+    pkts = make_packets(6000, 0xF00D + align_log2 + first_off)
+    expect = [O.rx_verify_ref(p, L4, L6, ones_comp=oracle.compute_ones_comp) for p in pkts]
+    st, l4 = run_packed_rx(pkts, align_log2, first_off, base_shift)
+    got = list(zip(st.tolist(), l4.tolist()))
+    bad = [(i, len(pkts[i]), got[i], expect[i]) for i in range(len(pkts)) if got[i] != tuple(expect[i])]
+    assert not bad, bad[:5]
+
+
+def test_packed_edge_datagrams_match_reference_path(oracle):
+    """Header-length edges (IHL 5..15 with short and empty segments), header-only UDP,
+    one-byte ICMP, IPv6 with empty segments and 0xff bodies up to 65535 bytes."""
+    pkts = []
+    for ihl in range(5, 16):
+        for size in (0, 1, 2, 3, 17, 31, 64, 65):
+            pkts.append(ipv4(6, tcp_seg(R4, L4, b"\xa5" * size), ihl=ihl))
+        pkts.append(ipv4(6, b"", ihl=ihl))
+        pkts.append(ipv4(17, b"", ihl=ihl))
+        pkts.append(ipv4(1, b"\x00", ihl=ihl))
+    pkts += [ipv6(6, b""), ipv6(58, b"\x01"), ipv4(1, icmp4(b"\xff" * 65000)), ipv6(6, tcp_seg(R6, L6, b"\xff" * 65400))]
+    pkts += [b"", b"\x45", b"\x60" * 39]
+    expect = [O.rx_verify_ref(p, L4, L6, ones_comp=oracle.compute_ones_comp) for p in pkts]
+    for first_off in (0, 16, 7):
+        st, l4 = run_packed_rx(pkts, 4, first_off)
+        got = list(zip(st.tolist(), l4.tolist()))
+        bad = [(i, len(pkts[i]), got[i], expect[i]) for i in range(len(pkts)) if got[i] != tuple(expect[i])]
+        assert not bad, (first_off, bad[:5])
+
+
+@pytest.mark.parametrize("name", ["c2_64B", "c5_imix"])
+def test_packed_full_size_equals_descriptor_entry(name):
+    """bench.py --op verify's batches (headers and checksums written on the device, every
+    1009th datagram corrupted): the packed entry's statuses equal rns_rx_verify_dev's, and
+    exactly the planted corruptions are rejected."""
+    from rustnetworkstack_amd.batch import rx_verify_packed
+    from rustnetworkstack_amd.workloads import LOCAL4, LOCAL6, make_verify_batch
+    lay = make_layout(name)
+    b = DeviceBatch(lay, DEV)
+    make_verify_batch(b)
+    b.launcher(packed=True)  # uploads blk_off / len16
+    ref = rx_verify(b.arena, b.off, b.length, LOCAL4, LOCAL6).clone()
+    got = rx_verify_packed(b.arena, b.blk_off, b.len16, LOCAL4, LOCAL6)
+    assert torch.equal(got, ref)
+    assert int(((got & _lib.RNS_RX_ACCEPT) == 0).sum().item()) == b.expected_bad
+    del b
+    torch.cuda.empty_cache()
