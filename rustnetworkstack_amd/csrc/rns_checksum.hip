@@ -1945,6 +1945,15 @@ __device__ __forceinline__ uint4 keep_first(uint4 v, uint32_t c)
 #define RNS_STREAM_OCC 8
 #endif
 constexpr int kStreamD = RNS_STREAM_D;
+#ifndef RNS_STREAM_BURST  // rows refilled together (1 = each row as it is consumed; D % BURST == 0)
+#define RNS_STREAM_BURST 1
+#endif
+constexpr int kStreamBurst = RNS_STREAM_BURST;
+static_assert(kStreamD % kStreamBurst == 0, "stream refill bursts");
+#ifndef RNS_STREAM_WPB  // waves (each with its own 64-packet block) per workgroup
+#define RNS_STREAM_WPB 1
+#endif
+constexpr int kStreamWpb = RNS_STREAM_WPB;
 
 // MODE kStashNone: the plain batch checksum (seed, optional complement, u16 out).
 // MODE kStashHead: receive verify (rns_rx_verify_packed_dev): the lanes that load a
@@ -1955,7 +1964,7 @@ constexpr int kStreamD = RNS_STREAM_D;
 #define RNS_STREAM_RX_OCC 6
 #endif
 template <int MODE, bool NT, bool BUF>
-__global__ __launch_bounds__(64, MODE == kStashHead ? RNS_STREAM_RX_OCC : RNS_STREAM_OCC) void csum_stream_kernel(
+__global__ __launch_bounds__(64 * kStreamWpb, MODE == kStashHead ? RNS_STREAM_RX_OCC : RNS_STREAM_OCC) void csum_stream_kernel(
     const CsumArgs a)
 {
     static_assert(MODE == kStashNone || MODE == kStashHead, "stream modes: plain, receive verify");
@@ -1964,17 +1973,23 @@ __global__ __launch_bounds__(64, MODE == kStashHead ? RNS_STREAM_RX_OCC : RNS_ST
     // entry bits: [31:18] row tag, [17] head chunk, [16:15] head index, [14] end chunk,
     // [13:8] packet, [7] first chunk, [3:0] valid bytes - 1 (end chunk)
     constexpr uint32_t kTagShift = 18, kHead = 1u << 17, kEnd = 1u << 14, kStart = 1u << 7;
-    __shared__ uint32_t tab[64];     // per row: the entry of the chunk lane l loads
-    __shared__ uint32_t pend[64];    // per packet: the region prefix through its last chunk
-    __shared__ uint32_t pstart[64];  // per packet: the region prefix before its first chunk
-    __shared__ uint4 stash[RX ? 64 * kNS : 1];
-    const uint32_t lane = threadIdx.x;
+    __shared__ uint32_t tab_w[kStreamWpb][64];     // per row: the entry of the chunk lane l loads
+    __shared__ uint32_t pend_w[kStreamWpb][64];    // per packet: the region prefix through its last chunk
+    __shared__ uint32_t pstart_w[kStreamWpb][64];  // per packet: the region prefix before its first chunk
+    __shared__ uint4 stash_w[kStreamWpb][RX ? 64 * kNS : 1];
+    const uint32_t wv = kStreamWpb == 1 ? 0u : threadIdx.x >> 6;
+    uint32_t *const tab = tab_w[wv];
+    uint32_t *const pend = pend_w[wv];
+    uint32_t *const pstart = pstart_w[wv];
+    uint4 *const stash = stash_w[wv];
+    const uint32_t lane = threadIdx.x & 63;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
     const uint64_t recs = buf_records(a);
     const uint64_t nblk = (static_cast<uint64_t>(a.n) + 63) >> 6;
 
-    for (uint64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    for (uint64_t blk = static_cast<uint64_t>(blockIdx.x) * kStreamWpb + wv; blk < nblk;
+         blk += static_cast<uint64_t>(gridDim.x) * kStreamWpb) {
         const uint64_t p = blk * 64 + lane;
         const bool live = p < a.n;
         const uint64_t q = live ? p : a.n - 1;
@@ -2064,7 +2079,13 @@ __global__ __launch_bounds__(64, MODE == kStashHead ? RNS_STREAM_RX_OCC : RNS_ST
                     // memory traffic).  Issued only after the row is consumed, so the loop-carried
                     // registers need no copy — a copy at the back edge waits for every load in flight.
                     __builtin_amdgcn_sched_barrier(0);
-                    issue(k + kStreamD, v[j]);
+                    if constexpr (kStreamBurst == 1) {
+                        issue(k + kStreamD, v[j]);
+                    } else if ((j + 1) % kStreamBurst == 0) {  // the group's rows refilled together
+#pragma unroll
+                        for (int i = 0; i < kStreamBurst; ++i)
+                            issue(k + 1 - kStreamBurst + i + kStreamD, v[j + 1 - kStreamBurst + i]);
+                    }
                     __builtin_amdgcn_sched_barrier(0);
                     const uint32_t inc = wave_incl_scan(s);
                     if (mark && (t & kStart))
@@ -2301,7 +2322,8 @@ int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
     const bool nt = (sh.variant & 2u) != 0, buf = buf_records(a) < kOobOffset;
     if (RNS_STREAM && a.align_mask >= 15u) {  // 16-byte-aligned packets: one wave streams each 64-packet block
         const uint64_t blocks = (static_cast<uint64_t>(a.n) + 63) / 64;
-        const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(blocks, 0x7FFFFFFFu))), block(64);
+        const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>((blocks + kStreamWpb - 1) / kStreamWpb, 0x7FFFFFFFu))),
+            block(64 * kStreamWpb);
         if (buf)
             hipLaunchKernelGGL((csum_stream_kernel<kStashNone, RNS_STREAM_NT != 0, true>), grid, block, 0, st, a);
         else
@@ -2726,7 +2748,8 @@ int rns_rx_verify_packed_dev(const uint8_t *d_arena, uint64_t arena_bytes, const
     a.local4_sum = be_sum(local_ipv4, 4);
     a.local6_sum = be_sum(local_ipv6, 16);
     const uint64_t blocks = (static_cast<uint64_t>(n) + 63) / 64;
-    const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(blocks, 0x7FFFFFFFu))), block(64);
+    const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>((blocks + kStreamWpb - 1) / kStreamWpb, 0x7FFFFFFFu))),
+        block(64 * kStreamWpb);
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (buf_records(a) < kOobOffset)
         hipLaunchKernelGGL((csum_stream_kernel<kStashHead, RNS_STREAM_NT != 0, true>), grid, block, 0, st, a);
