@@ -1950,6 +1950,9 @@ constexpr int kStreamD = RNS_STREAM_D;
 #endif
 constexpr int kStreamBurst = RNS_STREAM_BURST;
 static_assert(kStreamD % kStreamBurst == 0, "stream refill bursts");
+#ifndef RNS_STREAM_K  // A/B knob: 64-packet blocks per wave (grid capped); 0 = one wave per block
+#define RNS_STREAM_K 0
+#endif
 #ifndef RNS_STREAM_WPB  // waves (each with its own 64-packet block) per workgroup
 #define RNS_STREAM_WPB 1
 #endif
@@ -1988,14 +1991,28 @@ __global__ __launch_bounds__(64 * kStreamWpb, MODE == kStashHead ? RNS_STREAM_RX
     const uint64_t recs = buf_records(a);
     const uint64_t nblk = (static_cast<uint64_t>(a.n) + 63) >> 6;
 
-    for (uint64_t blk = static_cast<uint64_t>(blockIdx.x) * kStreamWpb + wv; blk < nblk;
-         blk += static_cast<uint64_t>(gridDim.x) * kStreamWpb) {
+    const uint64_t bstep = static_cast<uint64_t>(gridDim.x) * kStreamWpb;
+    // a block's descriptors (lengths, seeds, base offset), loaded one block ahead: a wave that
+    // owns several blocks (capped grid) has the next block's in registers when it gets there
+    uint32_t nx_len = 0, nx_seed = 0;
+    uint64_t nx_r0 = 0;
+    auto load_block = [&](uint64_t b) {  // branch-free: past the end re-reads the last block
+        const uint64_t bb = b < nblk ? b : nblk - 1;
+        const uint64_t pp = bb * 64 + lane;
+        const uint64_t qq = pp < a.n ? pp : a.n - 1;
+        nx_len = pp < a.n ? static_cast<uint32_t>(a.len16[qq]) : 0u;
+        nx_seed = (!RX && a.seed && pp < a.n) ? static_cast<uint32_t>(a.seed[qq]) : 0u;
+        nx_r0 = a.blk_off[bb];
+    };
+    load_block(static_cast<uint64_t>(blockIdx.x) * kStreamWpb + wv);
+    for (uint64_t blk = static_cast<uint64_t>(blockIdx.x) * kStreamWpb + wv; blk < nblk; blk += bstep) {
         const uint64_t p = blk * 64 + lane;
         const bool live = p < a.n;
-        const uint64_t q = live ? p : a.n - 1;
-        const uint32_t len = live ? static_cast<uint32_t>(a.len16[q]) : 0u;
-        const uint32_t seed = (!RX && a.seed && live) ? static_cast<uint32_t>(a.seed[q]) : 0u;
-        const uint64_t r0 = a.blk_off[blk] + a.base_adjust;               // the block's first packet
+        const uint32_t len = nx_len;
+        const uint32_t seed = nx_seed;
+        const uint64_t r0 = nx_r0 + a.base_adjust;                        // the block's first packet
+        if (bstep < nblk)
+            load_block(blk + bstep);
         const uint32_t pad = (len + a.align_mask) & ~a.align_mask;        // a multiple of 16
         const uint32_t incl = wave_incl_scan(pad);
         const uint32_t excl = incl - pad;
@@ -2322,7 +2339,8 @@ int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
     const bool nt = (sh.variant & 2u) != 0, buf = buf_records(a) < kOobOffset;
     if (RNS_STREAM && a.align_mask >= 15u) {  // 16-byte-aligned packets: one wave streams each 64-packet block
         const uint64_t blocks = (static_cast<uint64_t>(a.n) + 63) / 64;
-        const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>((blocks + kStreamWpb - 1) / kStreamWpb, 0x7FFFFFFFu))),
+        const uint64_t per_wg = static_cast<uint64_t>(kStreamWpb) * (RNS_STREAM_K > 0 ? RNS_STREAM_K : 1);
+        const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>((blocks + per_wg - 1) / per_wg, 0x7FFFFFFFu))),
             block(64 * kStreamWpb);
         if (buf)
             hipLaunchKernelGGL((csum_stream_kernel<kStashNone, RNS_STREAM_NT != 0, true>), grid, block, 0, st, a);
