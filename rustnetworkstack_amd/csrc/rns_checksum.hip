@@ -72,6 +72,7 @@ struct CsumArgs {
     const uint32_t *first;     // fragment chains: packet i = fragments [first[i], first[i+1]) (off/len = fragments)
     uint32_t n_frags;
     uint32_t chain_k;          // fragment chains: packets per lane (a wave owns 64*chain_k consecutive packets)
+    uint32_t len_hint;         // packed form: the caller's typical packet length (stream kernel packet sets)
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -1938,98 +1939,87 @@ __device__ __forceinline__ uint4 keep_first(uint4 v, uint32_t c)
     return v;
 }
 
+#ifndef RNS_STREAM  // A/B knob: 0 = the packed form always runs the class / rounds kernels
+#define RNS_STREAM 1
+#endif
+#ifndef RNS_STREAM_NT  // nontemporal loads in the stream kernel
+#define RNS_STREAM_NT 1
+#endif
 #ifndef RNS_STREAM_D  // rows (1 KiB loads) in flight per wave
 #define RNS_STREAM_D 4
 #endif
 #ifndef RNS_STREAM_OCC  // waves/SIMD bound
 #define RNS_STREAM_OCC 8
 #endif
+#ifndef RNS_STREAM_RX_OCC  // waves/SIMD bound of the receive-verify instantiation (its finish needs registers)
+#define RNS_STREAM_RX_OCC 6
+#endif
 constexpr int kStreamD = RNS_STREAM_D;
-#ifndef RNS_STREAM_BURST  // rows refilled together (1 = each row as it is consumed; D % BURST == 0)
-#define RNS_STREAM_BURST 1
-#endif
-constexpr int kStreamBurst = RNS_STREAM_BURST;
-static_assert(kStreamD % kStreamBurst == 0, "stream refill bursts");
-#ifndef RNS_STREAM_K  // A/B knob: 64-packet blocks per wave (grid capped); 0 = one wave per block
-#define RNS_STREAM_K 0
-#endif
-#ifndef RNS_STREAM_WPB  // waves (each with its own 64-packet block) per workgroup
-#define RNS_STREAM_WPB 1
-#endif
-constexpr int kStreamWpb = RNS_STREAM_WPB;
 
 // MODE kStashNone: the plain batch checksum (seed, optional complement, u16 out).
 // MODE kStashHead: receive verify (rns_rx_verify_packed_dev): the lanes that load a
 // datagram's first 4 chunks (64 bytes: every IPv4 header incl. options, the IPv6 header)
 // also copy them to an LDS stash, and the owner finishes exactly as the class kernel's
 // receive verify does (rx_finish).
-#ifndef RNS_STREAM_RX_OCC  // waves/SIMD bound of the receive-verify instantiation (its finish needs registers)
-#define RNS_STREAM_RX_OCC 6
+// KS: 64-packet sets per wave.  The wave's region is its KS*64 packets' bytes, streamed
+// as one row sequence: small packets (IMIX, ACKs) give a wave KS times the bytes, so the
+// per-wave start (descriptor load, first row latency) and end are paid KS times less
+// often.  Lane l owns packets 64*i + l of the wave's range (i < KS).
+#ifndef RNS_STREAM_OCC4  // waves/SIMD bound with 4 packet sets per wave (their descriptors need registers)
+#define RNS_STREAM_OCC4 6
 #endif
-template <int MODE, bool NT, bool BUF>
-__global__ __launch_bounds__(64 * kStreamWpb, MODE == kStashHead ? RNS_STREAM_RX_OCC : RNS_STREAM_OCC) void csum_stream_kernel(
+template <int MODE, int KS, bool NT, bool BUF>
+__global__ __launch_bounds__(64, MODE == kStashHead ? RNS_STREAM_RX_OCC : KS == 4 ? RNS_STREAM_OCC4 : RNS_STREAM_OCC) void
+csum_stream_kernel(
     const CsumArgs a)
 {
     static_assert(MODE == kStashNone || MODE == kStashHead, "stream modes: plain, receive verify");
+    static_assert(KS == 1 || KS == 2 || KS == 4, "packet sets per wave");
     constexpr bool RX = MODE == kStashHead;
     constexpr int kNS = RX ? 5 : 1;  // stash chunks per datagram (the unaligned path fills 5)
-    // entry bits: [31:18] row tag, [17] head chunk, [16:15] head index, [14] end chunk,
-    // [13:8] packet, [7] first chunk, [3:0] valid bytes - 1 (end chunk)
-    constexpr uint32_t kTagShift = 18, kHead = 1u << 17, kEnd = 1u << 14, kStart = 1u << 7;
-    __shared__ uint32_t tab_w[kStreamWpb][64];     // per row: the entry of the chunk lane l loads
-    __shared__ uint32_t pend_w[kStreamWpb][64];    // per packet: the region prefix through its last chunk
-    __shared__ uint32_t pstart_w[kStreamWpb][64];  // per packet: the region prefix before its first chunk
-    __shared__ uint4 stash_w[kStreamWpb][RX ? 64 * kNS : 1];
-    const uint32_t wv = kStreamWpb == 1 ? 0u : threadIdx.x >> 6;
-    uint32_t *const tab = tab_w[wv];
-    uint32_t *const pend = pend_w[wv];
-    uint32_t *const pstart = pstart_w[wv];
-    uint4 *const stash = stash_w[wv];
-    const uint32_t lane = threadIdx.x & 63;
+    constexpr uint32_t kNP = 64u * KS;
+    // entry bits: [31:17] row tag, [16] head chunk, [15:14] head index, [13] end chunk,
+    // [12] first chunk, [11:4] packet (of the wave's KS*64), [3:0] valid bytes - 1 (end chunk)
+    constexpr uint32_t kTagShift = 17, kHead = 1u << 16, kEnd = 1u << 13, kStart = 1u << 12;
+    __shared__ uint32_t tab[64];        // per row: the entry of the chunk lane l loads
+    __shared__ uint32_t pend[kNP];      // per packet: the region prefix through its last chunk
+    __shared__ uint32_t pstart[kNP];    // per packet: the region prefix before its first chunk
+    __shared__ uint4 stash[RX ? kNP * kNS : 1];
+    const uint32_t lane = threadIdx.x;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
     const uint64_t recs = buf_records(a);
-    const uint64_t nblk = (static_cast<uint64_t>(a.n) + 63) >> 6;
+    const uint64_t nunit = (static_cast<uint64_t>(a.n) + kNP - 1) / kNP;
 
-    const uint64_t bstep = static_cast<uint64_t>(gridDim.x) * kStreamWpb;
-    // a block's descriptors (lengths, seeds, base offset), loaded one block ahead: a wave that
-    // owns several blocks (capped grid) has the next block's in registers when it gets there
-    uint32_t nx_len = 0, nx_seed = 0;
-    uint64_t nx_r0 = 0;
-    auto load_block = [&](uint64_t b) {  // branch-free: past the end re-reads the last block
-        const uint64_t bb = b < nblk ? b : nblk - 1;
-        const uint64_t pp = bb * 64 + lane;
-        const uint64_t qq = pp < a.n ? pp : a.n - 1;
-        nx_len = pp < a.n ? static_cast<uint32_t>(a.len16[qq]) : 0u;
-        nx_seed = (!RX && a.seed && pp < a.n) ? static_cast<uint32_t>(a.seed[qq]) : 0u;
-        nx_r0 = a.blk_off[bb];
-    };
-    load_block(static_cast<uint64_t>(blockIdx.x) * kStreamWpb + wv);
-    for (uint64_t blk = static_cast<uint64_t>(blockIdx.x) * kStreamWpb + wv; blk < nblk; blk += bstep) {
-        const uint64_t p = blk * 64 + lane;
-        const bool live = p < a.n;
-        const uint32_t len = nx_len;
-        const uint32_t seed = nx_seed;
-        const uint64_t r0 = nx_r0 + a.base_adjust;                        // the block's first packet
-        if (bstep < nblk)
-            load_block(blk + bstep);
-        const uint32_t pad = (len + a.align_mask) & ~a.align_mask;        // a multiple of 16
-        const uint32_t incl = wave_incl_scan(pad);
-        const uint32_t excl = incl - pad;
-        const uint64_t start = r0 + excl;
-        const bool ok = start <= a.arena_bytes && len <= a.arena_bytes - start;
-        const bool nonempty = len != 0;
-        uint32_t mine = 0;
+    for (uint64_t u = blockIdx.x; u < nunit; u += gridDim.x) {
+        const uint64_t base = u * kNP;
+        const uint64_t r0 = a.blk_off[base >> 6] + a.base_adjust;  // the wave's first packet
+        uint32_t len[KS], seed[KS], excl[KS];
+        uint32_t total = 0;  // the region's bytes (a multiple of 16 on the stream path)
+#pragma unroll
+        for (int i = 0; i < KS; ++i) {
+            const uint64_t p = base + 64u * i + lane;
+            const uint64_t q = p < a.n ? p : a.n - 1;  // branch-free: past the end re-reads the last
+            len[i] = p < a.n ? static_cast<uint32_t>(a.len16[q]) : 0u;
+            seed[i] = (!RX && a.seed && p < a.n) ? static_cast<uint32_t>(a.seed[q]) : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < KS; ++i) {
+            const uint32_t pad = (len[i] + a.align_mask) & ~a.align_mask;
+            const uint32_t incl = wave_incl_scan(pad);
+            excl[i] = total + incl - pad;
+            total += __builtin_amdgcn_readlane(incl, 63);
+        }
+        uint32_t mine[KS];
         bool odd = false;
+#pragma unroll
+        for (int i = 0; i < KS; ++i)
+            mine[i] = 0;
 
         if ((r0 & 15) == 0) {
             // ---- stream path ----
-            const uint32_t total = __builtin_amdgcn_readlane(incl, 63);   // region bytes (multiple of 16)
             const uint32_t nrows = (total + 1023) >> 10;
-            const uint32_t c0 = excl >> 4;                                    // first chunk, region-relative
-            const uint32_t e = nonempty ? (excl + len - 1) >> 4 : 0xFFFFFFFFu;  // last chunk
-            const uint32_t ent = (lane << 8) | ((len - 1) & 15u);            // packet | valid bytes - 1
-            tab[lane] = 0xFFFFFFFFu;                                          // tag 0x3FFF: never a row
+            tab[lane] = 0xFFFFFFFFu;                                          // tag 0x7FFF: never a row
             wave_lds_fence();
             uint32_t carry = 0;
             uint4 v[kStreamD];
@@ -2057,36 +2047,44 @@ __global__ __launch_bounds__(64 * kStreamWpb, MODE == kStashHead ? RNS_STREAM_RX
                 for (int j = 0; j < kStreamD; ++j) {
                     const uint32_t k = k0 + j;
                     const uint32_t tag = k << kTagShift;
-                    // owners publish at the lanes that load their chunks in row k: the end chunk
-                    // (and, receive verify, the first 4 chunks)
-                    // (and its first chunk: padding chunks between packets, align_log2 > 4, belong
-                    // to no packet, so a packet's sum is its end prefix minus its own start prefix)
-                    if constexpr (RX) {
+                    // owners publish at the lanes that load their chunks in row k: the first chunk
+                    // (padding chunks between packets, align_log2 > 4, belong to no packet, so a
+                    // packet's sum is its end prefix minus its own start prefix), the last chunk
+                    // (its valid bytes) and, receive verify, the first 4 chunks (the stash)
 #pragma unroll
-                        for (uint32_t h = 0; h < 4; ++h) {
-                            const uint32_t c = c0 + h;
-                            if (nonempty && c <= e && (c >> 6) == k)
-                                tab[c & 63] = tag | kHead | (h << 15) | (h == 0 ? kStart : 0u) | (c == e ? kEnd : 0u) |
-                                              ent;
+                    for (int i = 0; i < KS; ++i) {
+                        const uint32_t c0 = excl[i] >> 4;
+                        const uint32_t e = (excl[i] + len[i] - 1) >> 4;
+                        const uint32_t ent = ((64u * i + lane) << 4) | ((len[i] - 1) & 15u);
+                        const bool ne = len[i] != 0;
+                        if constexpr (RX) {
+#pragma unroll
+                            for (uint32_t h = 0; h < 4; ++h) {
+                                const uint32_t c = c0 + h;
+                                if (ne && c <= e && (c >> 6) == k)
+                                    tab[c & 63] = tag | kHead | (h << 14) | (h == 0 ? kStart : 0u) |
+                                                  (c == e ? kEnd : 0u) | ent;
+                            }
+                            if (ne && e >= c0 + 4 && (e >> 6) == k)
+                                tab[e & 63] = tag | kEnd | ent;
+                        } else {
+                            if (ne && (c0 >> 6) == k)
+                                tab[c0 & 63] = tag | kStart | (c0 == e ? kEnd : 0u) | ent;
+                            if (ne && e != c0 && (e >> 6) == k)
+                                tab[e & 63] = tag | kEnd | ent;
                         }
-                        if (nonempty && e >= c0 + 4 && (e >> 6) == k)
-                            tab[e & 63] = tag | kEnd | ent;
-                    } else {
-                        if (nonempty && (c0 >> 6) == k)
-                            tab[c0 & 63] = tag | kStart | (c0 == e ? kEnd : 0u) | ent;
-                        if (nonempty && e != c0 && (e >> 6) == k)
-                            tab[e & 63] = tag | kEnd | ent;
                     }
                     wave_lds_fence();
                     const uint32_t t = tab[lane];
                     const bool mark = (t >> kTagShift) == k;
                     const bool is_end = mark && (t & kEnd);
+                    const uint32_t pk = (t >> 4) & 0xFFu;
                     uint4 x = v[j];
                     if (__ballot(is_end && (t & 15u) != 15u))  // a partial end chunk in this row
                         x = keep_first(x, is_end ? (t & 15u) + 1u : 16u);
                     if constexpr (RX) {
                         if (mark && (t & kHead))
-                            stash[((t >> 8) & 63u) * kNS + ((t >> 15) & 3u)] = x;
+                            stash[pk * kNS + ((t >> 14) & 3u)] = x;
                     }
                     uint32_t s = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
                     s = __builtin_amdgcn_sad_u16(x.y, 0, s);
@@ -2096,73 +2094,83 @@ __global__ __launch_bounds__(64 * kStreamWpb, MODE == kStashHead ? RNS_STREAM_RX
                     // memory traffic).  Issued only after the row is consumed, so the loop-carried
                     // registers need no copy — a copy at the back edge waits for every load in flight.
                     __builtin_amdgcn_sched_barrier(0);
-                    if constexpr (kStreamBurst == 1) {
-                        issue(k + kStreamD, v[j]);
-                    } else if ((j + 1) % kStreamBurst == 0) {  // the group's rows refilled together
-#pragma unroll
-                        for (int i = 0; i < kStreamBurst; ++i)
-                            issue(k + 1 - kStreamBurst + i + kStreamD, v[j + 1 - kStreamBurst + i]);
-                    }
+                    issue(k + kStreamD, v[j]);
                     __builtin_amdgcn_sched_barrier(0);
                     const uint32_t inc = wave_incl_scan(s);
                     if (mark && (t & kStart))
-                        pstart[(t >> 8) & 63u] = carry + inc - s;
+                        pstart[pk] = carry + inc - s;
                     if (is_end)
-                        pend[(t >> 8) & 63u] = carry + inc;
+                        pend[pk] = carry + inc;
                     carry += __builtin_amdgcn_readlane(inc, 63);
                     wave_lds_fence();
                 }
             }
             // a packet's sum: the region prefix through its last chunk minus the prefix before its
             // first (u32 differences: exact, a packet's LE sum is < 2^32)
-            mine = nonempty ? pend[lane] - pstart[lane] : 0u;
+#pragma unroll
+            for (int i = 0; i < KS; ++i)
+                mine[i] = len[i] ? pend[64u * i + lane] - pstart[64u * i + lane] : 0u;
         } else {
             // ---- unaligned region (rare): the whole wave sums one packet at a time ----
-            uint64_t todo = __ballot(nonempty && ok);
-            while (todo) {
-                const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
-                todo &= todo - 1;
-                const uint64_t st = (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start >> 32), o))
-                                     << 32) | __builtin_amdgcn_readlane(static_cast<uint32_t>(start), o);
-                const uint32_t L = __builtin_amdgcn_readlane(len, o);
-                const Pkt k = make_pkt(st, L);
-                uint32_t acc = 0;
-                for (uint32_t cc = 0; cc < k.nch; cc += 64) {
-                    uint4 w[1];
-                    issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, w);
-                    mask_edges<64, 1, 1>(k, cc + lane, w);
-                    if constexpr (RX) {
-                        if (cc == 0 && lane < static_cast<uint32_t>(kNS))
-                            stash[o * kNS + lane] = lane < k.nch ? w[0] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < KS; ++i) {
+                const uint64_t start = r0 + excl[i];
+                const bool ok = start <= a.arena_bytes && len[i] <= a.arena_bytes - start;
+                uint64_t todo = __ballot(len[i] != 0 && ok);
+                while (todo) {
+                    const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
+                    todo &= todo - 1;
+                    const uint64_t st =
+                        (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start >> 32), o)) << 32) |
+                        __builtin_amdgcn_readlane(static_cast<uint32_t>(start), o);
+                    const uint32_t L = __builtin_amdgcn_readlane(len[i], o);
+                    const Pkt k = make_pkt(st, L);
+                    uint32_t acc = 0;
+                    for (uint32_t cc = 0; cc < k.nch; cc += 64) {
+                        uint4 w[1];
+                        issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, w);
+                        mask_edges<64, 1, 1>(k, cc + lane, w);
+                        if constexpr (RX) {
+                            if (cc == 0 && lane < static_cast<uint32_t>(kNS))
+                                stash[(64u * i + o) * kNS + lane] = lane < k.nch ? w[0] : make_uint4(0, 0, 0, 0);
+                        }
+                        acc = sum_le<1, 1>(w, acc);
                     }
-                    acc = sum_le<1, 1>(w, acc);
+                    const uint32_t sum = group_allreduce<64>(acc);
+                    mine[i] = lane == o ? sum : mine[i];
                 }
-                const uint32_t sum = group_allreduce<64>(acc);
-                mine = lane == o ? sum : mine;
             }
-            odd = start & 1;
+            odd = r0 & 1;  // every packet of the range shares the region start's misalignment
         }
         wave_lds_fence();
-        if constexpr (RX) {
-            uint32_t l4_res = 0;
-            const uint8_t stv = rx_finish<kNS>(a, stash + lane * kNS, mine, static_cast<uint32_t>(start & 15), len, odd,
-                                               false, live && ok && nonempty, l4_res);
-            if (live) {
-                a.status[p] = stv;
-                if (a.l4_out)
-                    a.l4_out[p] = static_cast<uint16_t>(l4_res);
-            }
-        } else {
-            const uint16_t res = finalize_bits(mine, odd, false, seed, ok, a.flags);
-            if (live)
-                a.out[p] = res;  // 64 consecutive u16: one 128-byte store
-            if (a.bad) {
-                const uint64_t rejected = __ballot(live && !ok);
-                if (rejected && lane == 0)
-                    atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
+#pragma unroll
+        for (int i = 0; i < KS; ++i) {
+            const uint64_t p = base + 64u * i + lane;
+            const bool live = p < a.n;
+            const uint64_t start = r0 + excl[i];
+            const bool ok = start <= a.arena_bytes && len[i] <= a.arena_bytes - start;
+            if constexpr (RX) {
+                uint32_t l4_res = 0;
+                const uint8_t stv = rx_finish<kNS>(a, stash + (64u * i + lane) * kNS, mine[i],
+                                                   static_cast<uint32_t>(start & 15), len[i], odd, false,
+                                                   live && ok && len[i] != 0, l4_res);
+                if (live) {
+                    a.status[p] = stv;
+                    if (a.l4_out)
+                        a.l4_out[p] = static_cast<uint16_t>(l4_res);
+                }
+            } else {
+                const uint16_t res = finalize_bits(mine[i], odd, false, seed[i], ok, a.flags);
+                if (live)
+                    a.out[p] = res;  // 64 consecutive u16: one 128-byte store
+                if (a.bad) {
+                    const uint64_t rejected = __ballot(live && !ok);
+                    if (rejected && lane == 0)
+                        atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
+                }
             }
         }
-        wave_lds_fence();  // the next block rewrites tab / pend / stash
+        wave_lds_fence();  // the next range rewrites tab / pend / stash
     }
 }
 
@@ -2328,26 +2336,51 @@ Shape pick_shape(uint32_t len_hint)
 // The packed form's kernels (separate instantiations, so the explicit-descriptor
 // kernels carry no packed-form code): the mixed kernel, or for tiny packets the
 // rounds kernel with pick_shape's G=4, U=1 shape.
-#ifndef RNS_STREAM  // A/B knob: 0 = the packed form always runs the class / rounds kernels
-#define RNS_STREAM 1
+// Packed-form stream launch: KS from the typical packet length (A/B: -DRNS_STREAM_KS=n forces n).
+#ifndef RNS_STREAM_KS
+#define RNS_STREAM_KS 0
 #endif
-#ifndef RNS_STREAM_NT  // nontemporal loads in the stream kernel
-#define RNS_STREAM_NT 1
-#endif
+inline int stream_sets(uint32_t len_hint)
+{
+    if (RNS_STREAM_KS > 0)
+        return RNS_STREAM_KS;
+    return len_hint != 0 && len_hint <= 400 ? 4 : len_hint != 0 && len_hint <= 1200 ? 2 : 1;
+}
+
+template <int MODE>
+int launch_stream(const CsumArgs &a, int ks, hipStream_t st)
+{
+    const bool buf = buf_records(a) < kOobOffset;
+    const uint64_t units = (static_cast<uint64_t>(a.n) + 64u * ks - 1) / (64u * ks);
+    const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(units, 0x7FFFFFFFu))), block(64);
+    constexpr bool NT = RNS_STREAM_NT != 0;
+#define RNS_LAUNCH_STREAM(K)                                                                       \
+    do {                                                                                           \
+        if (buf)                                                                                   \
+            hipLaunchKernelGGL((csum_stream_kernel<MODE, K, NT, true>), grid, block, 0, st, a);    \
+        else                                                                                       \
+            hipLaunchKernelGGL((csum_stream_kernel<MODE, K, NT, false>), grid, block, 0, st, a);   \
+    } while (0)
+    if constexpr (MODE == kStashNone) {
+        if (ks == 4)
+            RNS_LAUNCH_STREAM(4);
+        else if (ks == 2)
+            RNS_LAUNCH_STREAM(2);
+        else
+            RNS_LAUNCH_STREAM(1);
+    } else {
+        (void)ks;  // receive verify: one set per wave (its stash is 5 chunks per datagram)
+        RNS_LAUNCH_STREAM(1);
+    }
+#undef RNS_LAUNCH_STREAM
+    return hip_status(hipGetLastError());
+}
+
 int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
 {
     const bool nt = (sh.variant & 2u) != 0, buf = buf_records(a) < kOobOffset;
-    if (RNS_STREAM && a.align_mask >= 15u) {  // 16-byte-aligned packets: one wave streams each 64-packet block
-        const uint64_t blocks = (static_cast<uint64_t>(a.n) + 63) / 64;
-        const uint64_t per_wg = static_cast<uint64_t>(kStreamWpb) * (RNS_STREAM_K > 0 ? RNS_STREAM_K : 1);
-        const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>((blocks + per_wg - 1) / per_wg, 0x7FFFFFFFu))),
-            block(64 * kStreamWpb);
-        if (buf)
-            hipLaunchKernelGGL((csum_stream_kernel<kStashNone, RNS_STREAM_NT != 0, true>), grid, block, 0, st, a);
-        else
-            hipLaunchKernelGGL((csum_stream_kernel<kStashNone, RNS_STREAM_NT != 0, false>), grid, block, 0, st, a);
-        return hip_status(hipGetLastError());
-    }
+    if (RNS_STREAM && a.align_mask >= 15u)  // 16-byte-aligned packets: the stream kernel
+        return launch_stream<kStashNone>(a, stream_sets(a.len_hint), st);
     const uint64_t batches = (static_cast<uint64_t>(a.n) + 63) / 64;  // one wave per 64 packets
     const uint64_t wpb = ((sh.variant & 4u) ? kMixedBlock<false> : kBlock) / 64;  // waves per workgroup
     uint64_t blocks = (batches + wpb - 1) / wpb;
@@ -2544,6 +2577,7 @@ int rns_csum_batch_packed_dev(const uint8_t *d_arena, uint64_t arena_bytes, cons
     a.bad = d_bad;
     a.n = n;
     a.flags = flags;
+    a.len_hint = len_hint;
     return dispatch_packed(a, sh, static_cast<hipStream_t>(stream));
 }
 
@@ -2765,15 +2799,7 @@ int rns_rx_verify_packed_dev(const uint8_t *d_arena, uint64_t arena_bytes, const
     a.l4_out = d_l4_sum;
     a.local4_sum = be_sum(local_ipv4, 4);
     a.local6_sum = be_sum(local_ipv6, 16);
-    const uint64_t blocks = (static_cast<uint64_t>(n) + 63) / 64;
-    const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>((blocks + kStreamWpb - 1) / kStreamWpb, 0x7FFFFFFFu))),
-        block(64 * kStreamWpb);
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    if (buf_records(a) < kOobOffset)
-        hipLaunchKernelGGL((csum_stream_kernel<kStashHead, RNS_STREAM_NT != 0, true>), grid, block, 0, st, a);
-    else
-        hipLaunchKernelGGL((csum_stream_kernel<kStashHead, RNS_STREAM_NT != 0, false>), grid, block, 0, st, a);
-    return hip_status(hipGetLastError());
+    return launch_stream<kStashHead>(a, 1, static_cast<hipStream_t>(stream));
 }
 
 int rns_tx_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off, const uint32_t *d_len,
