@@ -102,8 +102,9 @@ def parse_args(argv=None):
     args = p.parse_args(argv)
     if args.shape and args.desc in ("32", "packed"):
         p.error("--shape overrides take 64-bit descriptors (--desc 64 or auto)")
-    if args.op == "verify" and (args.shape or args.desc not in ("auto", "64")):
-        p.error("--op verify takes 64-bit descriptors and the receive kernel's own shape")
+    if args.op == "verify" and (args.shape or args.desc not in ("auto", "64", "packed")):
+        p.error("--op verify takes the packed form (rns_rx_verify_packed_dev; auto) or 64-bit descriptors "
+                "(rns_rx_verify_dev) and the receive kernel's own shape")
     args.shard_rw = None
     if args.shard:
         try:
@@ -349,14 +350,18 @@ class GpuEngine:
             small = self.layout.arena_bytes + 16 < 2 ** 32
             jumbo = self.layout.mean_len > 2500  # pick_shape's group kernel: no wave batches, no packed form
             form = "64" if shape is not None else ("packed" if not jumbo else ("32" if small else "64"))
-        if op == "verify":  # the receive kernel reads 64-bit descriptors
+        if op == "verify":  # packed receive arena (16-byte-aligned datagrams): the stream kernel; else 64-bit
             from rustnetworkstack_amd.workloads import make_verify_batch
-            form = "64"
+            aligned = self.layout.n == 0 or int(self.layout.off[0]) % 16 == 0
+            form = "packed" if compact in ("auto", "packed") and aligned else "64"
             for b in self.batches:
                 make_verify_batch(b)
+                if form == "packed":
+                    b.launcher(packed=True)  # uploads blk_off / len16
         self.form = form
         self.compact = form == "32"
         self.packed = form == "packed"
+        self.verify_packed = op == "verify" and self.packed
         for b in self.batches:  # bind every rotating batch (and upload its descriptors) before any timing
             if op == "csum":
                 b.launcher(complement=True, shape=shape, compact=self.compact, packed=self.packed)
@@ -377,8 +382,10 @@ class GpuEngine:
         return self.layout.payload_bytes
 
     def _verify_call(self, b):
-        from rustnetworkstack_amd.batch import rx_verify
+        from rustnetworkstack_amd.batch import rx_verify, rx_verify_packed
         from rustnetworkstack_amd.workloads import LOCAL4, LOCAL6
+        if self.verify_packed:
+            return lambda: rx_verify_packed(b.arena, b.blk_off, b.len16, LOCAL4, LOCAL6, status=b.status)
         return lambda: rx_verify(b.arena, b.off, b.length, LOCAL4, LOCAL6, status=b.status)  # current stream
 
     def step(self):
@@ -484,8 +491,11 @@ class GpuEngine:
     def kernel_name(self) -> str:
         from rustnetworkstack_amd import _lib
         if self.op == "verify":
+            if self.verify_packed:
+                return "csum_stream_kernel<RX> (rns_rx_verify_packed_dev: 1 KiB rows + header stash)"
             return "csum_mixed_kernel<RX> (rns_rx_verify_dev: class-sorted data pass + header stash)"
-        if self.packed and self.layout.n and int(self.layout.off[0]) % 16 == 0:
+        mean = self.layout.mean_len
+        if self.packed and self.layout.n and int(self.layout.off[0]) % 16 == 0 and 112 < mean <= 1200:
             return ("csum_stream_kernel (packed form, 16-byte-aligned packets: one wave streams each 64-packet "
                     "block as 1 KiB rows, prefix sums per packet)")
         return _lib.load().rns_csum_shape_name(int(round(self.layout.mean_len))).decode()
@@ -721,7 +731,7 @@ def main(argv=None):
     # payload read + the result written: u16 sum (csum) or u8 status (verify)
     algo_bytes = engine.payload_bytes + (1 if verify else 2) * engine.n
     # descriptor bytes a launch reads (seeds included): packed 2 B length + 8 B per 64 packets
-    desc_bytes = (engine.n * (2 + 2) + 8 * ((engine.n + 63) // 64) if engine.packed
+    desc_bytes = (engine.n * (2 + (0 if verify else 2)) + 8 * ((engine.n + 63) // 64) if engine.packed
                   else engine.n * ((4 if engine.compact else 8) + 4 + (0 if verify else 2)))
     kernel_us = kernel_ms * 1e3
     achieved = algo_bytes / (kernel_us * 1e-6) / 1e9
@@ -756,10 +766,13 @@ def main(argv=None):
             "batch": "one batch sharded by packet index across ranks" if strong else "a full batch per rank",
             "parallelism": f"packet shards x{dist.world}, no data-path collective in `value`",
             "kernel_shape": list(shape) if shape else "auto",
-            "descriptors": {"32": "u32 offset + u32 length + u16 seed (rns_csum_batch_dev_off32)",
-                            "64": "u64 offset + u32 length + u16 seed (rns_csum_batch_dev)",
-                            "packed": "packed: u16 length + u16 seed per packet, u64 offset per 64 packets "
-                                      "(rns_csum_batch_packed_dev)"}[engine.form],
+            "descriptors": ({"64": "u64 offset + u32 length per datagram (rns_rx_verify_dev)",
+                             "packed": "packed: u16 length per datagram, u64 offset per 64 datagrams "
+                                       "(rns_rx_verify_packed_dev)"} if verify else
+                            {"32": "u32 offset + u32 length + u16 seed (rns_csum_batch_dev_off32)",
+                             "64": "u64 offset + u32 length + u16 seed (rns_csum_batch_dev)",
+                             "packed": "packed: u16 length + u16 seed per packet, u64 offset per 64 packets "
+                                       "(rns_csum_batch_packed_dev)"})[engine.form],
             "rotating_batches": len(engine.batches),
             "rotation": ("one batch per graph stream at least, each with its own bytes: steps that may run at the same "
                          "time never read the same arena" if use_graph and args.graph_streams > 1 else

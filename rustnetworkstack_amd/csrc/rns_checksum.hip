@@ -1965,11 +1965,8 @@ constexpr int kStreamD = RNS_STREAM_D;
 // as one row sequence: small packets (IMIX, ACKs) give a wave KS times the bytes, so the
 // per-wave start (descriptor load, first row latency) and end are paid KS times less
 // often.  Lane l owns packets 64*i + l of the wave's range (i < KS).
-#ifndef RNS_STREAM_OCC4  // waves/SIMD bound with 4 packet sets per wave (their descriptors need registers)
-#define RNS_STREAM_OCC4 6
-#endif
 template <int MODE, int KS, bool NT, bool BUF>
-__global__ __launch_bounds__(64, MODE == kStashHead ? RNS_STREAM_RX_OCC : KS == 4 ? RNS_STREAM_OCC4 : RNS_STREAM_OCC) void
+__global__ __launch_bounds__(64, MODE == kStashHead ? RNS_STREAM_RX_OCC : KS == 4 ? 5 : RNS_STREAM_OCC) void
 csum_stream_kernel(
     const CsumArgs a)
 {
@@ -2174,6 +2171,227 @@ csum_stream_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// v5: fragment chains as a stream (util.rs:112-119 over NetBuffer fragments,
+// buf.rs:466-487).  A wave owns 64 consecutive packets; their fragments are taken 64
+// at a time (a SUB-BLOCK), and the sub-block's fragments are streamed as ONE sequence
+// of 16-byte chunks — fragment j's chunks, then fragment j+1's, wherever each lies in
+// the arena — in rows of 64 chunks, D rows in flight, so a 512-byte fragment is half a
+// row instead of a size-class unit of its own.  Per row a lane finds the fragment its
+// chunk belongs to with a max-scan of the fragments' start marks (fragments publish
+// their first virtual chunk), loads the chunk from that fragment's address, and zeroes
+// the bytes before the fragment start / after its end.  Prefix sums over the row give
+// each fragment's LE word sum (pend - pstart, exact for fragments <= 128 KiB), which is
+// folded and byte-swapped by the fragment's start parity (RFC 1071 §2(B)) into the
+// reference's per-fragment BE sum mod 0xffff; each packet's owner lane then folds its
+// fragments in order, exactly as util.rs:114-116 does.  A sub-block holding a fragment
+// longer than 128 KiB (the reference's u32 can wrap) sums its fragments one at a time
+// with the exact big-endian path instead.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v)
+{
+    uint32_t x = max(v, dpp_or_zero<0x111>(v));       // row_shr:1
+    x = max(x, dpp_or_zero<0x112>(v));                // row_shr:2
+    x = max(x, dpp_or_zero<0x113>(v));                // row_shr:3
+    x = max(x, dpp_or_zero<0x114, 0xF, 0xE>(x));      // row_shr:4, banks 1-3
+    x = max(x, dpp_or_zero<0x118, 0xF, 0xC>(x));      // row_shr:8, banks 2-3
+    x = max(x, dpp_or_zero<0x142, 0xA, 0xF>(x));      // row_bcast:15 into rows 1 and 3
+    x = max(x, dpp_or_zero<0x143, 0xC, 0xF>(x));      // row_bcast:31 into rows 2 and 3
+    return x;
+}
+
+#ifndef RNS_CHAIN_STREAM_OCC
+#define RNS_CHAIN_STREAM_OCC 6
+#endif
+
+template <bool NT, bool BUF>
+__global__ __launch_bounds__(64, RNS_CHAIN_STREAM_OCC) void csum_chain_stream_kernel(const CsumArgs a)
+{
+    __shared__ uint32_t mark[64];    // per row: the fragment (j+1, tagged) whose first chunk lane l loads
+    __shared__ uint4 finfo[64];      // per fragment of the sub-block: address, first virtual chunk, bounds
+    __shared__ uint32_t pend[64];    // per fragment: the prefix through its last chunk
+    __shared__ uint32_t pstart[64];  // per fragment: the prefix before its first chunk
+    const uint32_t lane = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
+    const uint64_t recs = buf_records(a);
+    constexpr uint32_t kBad = 0x80000000u;
+
+    for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * 64; base < a.n;
+         base += static_cast<uint64_t>(gridDim.x) * 64) {
+        const uint64_t p = base + lane;
+        const bool live = p < a.n;
+        uint32_t f0 = live ? a.first[p] : 0u, f1 = live ? a.first[p + 1] : 0u;
+        const bool rng_ok = f0 <= f1 && f1 <= a.n_frags;
+        if (!rng_ok)
+            f0 = f1 = 0;
+        uint32_t acc = ((a.seed && live) ? static_cast<uint32_t>(a.seed[p]) : 0u) | (rng_ok ? 0u : kBad);  // util.rs:113
+        const uint32_t F0 = wave_min_u32(f0 < f1 ? f0 : 0xFFFFFFFFu);
+        const uint32_t F1 = wave_max_u32(f0 < f1 ? f1 : 0u);
+        for (uint64_t fb = F0; fb < F1; fb += 64) {
+            const uint64_t f = fb + lane;
+            const bool has = f < F1;
+            const uint64_t foff = has ? a.off[f] + a.base_adjust : 0;
+            const uint32_t flen = has ? a.len[f] : 0u;
+            const bool fok = foff <= a.arena_bytes && flen <= a.arena_bytes - foff;
+            const uint32_t fs = static_cast<uint32_t>(foff & 15);
+            const bool big = fok && flen > kNoWrapBytes;
+            uint32_t g = 0;  // the fragment's folded BE sum (big: the exact BE sum mod 2^32)
+            if (!__ballot(big)) {
+                // ---- stream path ----
+                const uint32_t nch = (fok && flen) ? (fs + flen + 15) >> 4 : 0u;
+                const uint32_t vincl = wave_incl_scan(nch);
+                const uint32_t vex = vincl - nch;  // first virtual chunk
+                const uint32_t total = __builtin_amdgcn_readlane(vincl, 63);
+                const uint32_t nrows = (total + 63) >> 6;
+                finfo[lane] = make_uint4(static_cast<uint32_t>(foff & ~15ull), static_cast<uint32_t>(foff >> 32), vex,
+                                         fs | ((nch ? ((fs + flen - 1) & 15u) + 1u : 16u) << 8) | (nch << 13));
+                mark[lane] = 0xFFFFFFFFu;
+                wave_lds_fence();
+                uint32_t active = 0;  // j+1 of the fragment running at the end of the last looked-up row
+                uint32_t carry = 0;
+                // row k: which fragment each lane's chunk belongs to; its address and byte bounds
+                auto lookup = [&](uint32_t k, uint32_t &info) -> uint64_t {
+                    if (nch && (vex >> 6) == k)
+                        mark[vex & 63] = (k << 7) | (lane + 1);
+                    wave_lds_fence();
+                    const uint32_t m = mark[lane];
+                    const uint32_t jj = max(wave_incl_max((m >> 7) == k ? (m & 127u) : 0u), active);
+                    active = __builtin_amdgcn_readlane(jj, 63);
+                    const uint32_t v = (k << 6) + lane;
+                    const bool valid = jj != 0 && v < total;
+                    const uint4 fi = finfo[valid ? jj - 1 : 0];
+                    wave_lds_fence();
+                    const uint32_t rel = v - fi.z;
+                    const uint32_t lo = rel == 0 ? (fi.w & 15u) : 0u;
+                    const uint32_t last = (fi.w >> 13) - 1;
+                    const uint32_t hi = rel == last ? ((fi.w >> 8) & 31u) : 16u;
+                    info = valid ? 1u | ((jj - 1) << 1) | (lo << 7) | (hi << 11) | (rel == 0 ? 1u << 16 : 0u) |
+                                       (rel == last ? 1u << 17 : 0u)
+                                 : 0u;
+                    return valid ? ((static_cast<uint64_t>(fi.y) << 32) | fi.x) + (static_cast<uint64_t>(rel) << 4)
+                                 : recs;  // past the arena: no load
+                };
+                auto issue = [&](uint64_t off, uint4 &dst) {
+                    const bool in = off + 16 <= recs;
+                    if constexpr (BUF) {
+                        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(
+                            rsrc, in ? static_cast<uint32_t>(off) : kOobOffset, 0, NT ? kNtAux : 0);
+                        dst = make_uint4(x.x, x.y, x.z, x.w);
+                    } else {
+                        const uint4 x = load_chunk<NT>(a.arena + (in ? off : 0));
+                        dst = in ? x : make_uint4(0, 0, 0, 0);
+                    }
+                };
+                uint4 v[kStreamD];
+                uint32_t inf[kStreamD];
+#pragma unroll
+                for (int j = 0; j < kStreamD; ++j) {
+                    issue(lookup(j, inf[j]), v[j]);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                for (uint32_t k0 = 0; k0 < nrows; k0 += kStreamD) {
+#pragma unroll
+                    for (int j = 0; j < kStreamD; ++j) {
+                        const uint32_t k = k0 + j;
+                        const uint32_t in = inf[j];
+                        uint4 x = v[j];
+                        const uint32_t lo = (in >> 7) & 15u, hi = (in >> 11) & 31u;
+                        if (__ballot(lo != 0 || hi != 16)) {  // a fragment starts or ends inside a chunk here
+                            x.x = keep_bytes(x.x, static_cast<int>(lo), static_cast<int>(hi), 0);
+                            x.y = keep_bytes(x.y, static_cast<int>(lo), static_cast<int>(hi), 4);
+                            x.z = keep_bytes(x.z, static_cast<int>(lo), static_cast<int>(hi), 8);
+                            x.w = keep_bytes(x.w, static_cast<int>(lo), static_cast<int>(hi), 12);
+                        }
+                        uint32_t s = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
+                        s = __builtin_amdgcn_sad_u16(x.y, 0, s);
+                        s = __builtin_amdgcn_sad_u16(x.z, 0, s);
+                        s = __builtin_amdgcn_sad_u16(x.w, 0, s);
+                        s = (in & 1u) ? s : 0u;
+                        __builtin_amdgcn_sched_barrier(0);
+                        issue(lookup(k + kStreamD, inf[j]), v[j]);
+                        __builtin_amdgcn_sched_barrier(0);
+                        const uint32_t inc = wave_incl_scan(s);
+                        const uint32_t jl = (in >> 1) & 63u;
+                        if (in & (1u << 16))
+                            pstart[jl] = carry + inc - s;
+                        if (in & (1u << 17))
+                            pend[jl] = carry + inc;
+                        carry += __builtin_amdgcn_readlane(inc, 63);
+                        wave_lds_fence();
+                    }
+                }
+                const uint32_t w = nch ? pend[lane] - pstart[lane] : 0u;  // LE word sum, exact
+                const uint32_t x = fold16(w);
+                g = (foff & 1) ? x : (((x & 0xff) << 8) | (x >> 8));
+                wave_lds_fence();
+            } else {
+                // ---- a fragment past 128 KiB in this sub-block: one fragment at a time ----
+                uint64_t todo = __ballot(fok && flen != 0);
+                while (todo) {
+                    const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
+                    todo &= todo - 1;
+                    const uint64_t st =
+                        (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(foff >> 32), o)) << 32) |
+                        __builtin_amdgcn_readlane(static_cast<uint32_t>(foff), o);
+                    const uint32_t L = __builtin_amdgcn_readlane(flen, o);
+                    const Pkt k = make_pkt(st, L);
+                    uint32_t hs = 0, ls = 0, le = 0;
+                    for (uint32_t cc = 0; cc < k.nch; cc += 64) {
+                        uint4 wv[1];
+                        issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, wv);
+                        mask_edges<64, 1, 1>(k, cc + lane, wv);
+                        if (k.big)
+                            sum_be<1, 1>(wv, (st & 1) ? 0x01000100u : 0x00010001u, hs, ls);
+                        else
+                            le = sum_le<1, 1>(wv, le);
+                    }
+                    const uint32_t sum = group_allreduce<64>(k.big ? (hs << 8) + ls : le);
+                    uint32_t gv = sum;
+                    if (!k.big) {
+                        const uint32_t xx = fold16(sum);
+                        gv = (st & 1) ? xx : (((xx & 0xff) << 8) | (xx >> 8));
+                    }
+                    g = lane == o ? gv : g;
+                }
+            }
+            // owner lanes: each packet's fragments inside [fb, fb + 64), in order (util.rs:114-116)
+            const uint32_t gflag = (big ? 1u : 0u) | ((has && !fok) ? 2u : 0u);
+            uint64_t t = max(static_cast<uint64_t>(f0), fb);
+            const uint64_t hi = min(static_cast<uint64_t>(f1), fb + 64);
+            while (__ballot(t < hi)) {
+                const bool act = t < hi;
+                const int src = act ? static_cast<int>(t - fb) : 0;
+                const uint32_t gv = static_cast<uint32_t>(__shfl(static_cast<int>(g), src, 64));
+                const uint32_t fv = static_cast<uint32_t>(__shfl(static_cast<int>(gflag), src, 64));
+                if (act) {
+                    const uint32_t bad = (acc & kBad) | ((fv & 2u) ? kBad : 0u);
+                    uint32_t s = (acc & 0xffffu) + gv;  // big: util.rs:89-99 mod 2^32; else <= 0x1fffe
+                    if (fv & 1u) {
+                        while (s > 0xffff)  // util.rs:101-103
+                            s = (s & 0xffff) + (s >> 16);
+                    } else {
+                        s = (s & 0xffff) + (s >> 16);  // one end-around step folds it
+                    }
+                    acc = s | bad;
+                    ++t;
+                }
+            }
+        }
+        uint32_t r = acc & 0xffffu;
+        if (a.flags & RNS_FLAG_COMPLEMENT)
+            r ^= 0xffff;
+        const bool ok = !(acc & kBad);
+        if (live)
+            a.out[p] = static_cast<uint16_t>(ok ? r : 0u);  // 64 consecutive u16: one 128-byte store
+        if (a.bad) {
+            const uint64_t rejected = __ballot(live && !ok);
+            if (rejected && lane == 0)
+                atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
+        }
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void splitmix64_fill_kernel(uint8_t *buf, uint64_t nbytes, uint64_t seed)
 {
     const uint64_t nwords = (nbytes + 7) / 8;
@@ -2336,17 +2554,12 @@ Shape pick_shape(uint32_t len_hint)
 // The packed form's kernels (separate instantiations, so the explicit-descriptor
 // kernels carry no packed-form code): the mixed kernel, or for tiny packets the
 // rounds kernel with pick_shape's G=4, U=1 shape.
-// Packed-form stream launch: KS from the typical packet length (A/B: -DRNS_STREAM_KS=n forces n).
-#ifndef RNS_STREAM_KS
-#define RNS_STREAM_KS 0
+// Packed-form stream launch.  One 64-packet set per wave: 2 or 4 sets per wave (one row
+// stream over 128-256 packets) measured no faster on IMIX, 40-byte and 576-byte batches,
+// and slower where their descriptors spill (profiles/r03_stream_ab.json, session r03f).
+#ifndef RNS_STREAM_KS  // A/B knob: packet sets per wave
+#define RNS_STREAM_KS 1
 #endif
-inline int stream_sets(uint32_t len_hint)
-{
-    if (RNS_STREAM_KS > 0)
-        return RNS_STREAM_KS;
-    return len_hint != 0 && len_hint <= 400 ? 4 : len_hint != 0 && len_hint <= 1200 ? 2 : 1;
-}
-
 template <int MODE>
 int launch_stream(const CsumArgs &a, int ks, hipStream_t st)
 {
@@ -2361,15 +2574,11 @@ int launch_stream(const CsumArgs &a, int ks, hipStream_t st)
         else                                                                                       \
             hipLaunchKernelGGL((csum_stream_kernel<MODE, K, NT, false>), grid, block, 0, st, a);   \
     } while (0)
-    if constexpr (MODE == kStashNone) {
-        if (ks == 4)
-            RNS_LAUNCH_STREAM(4);
-        else if (ks == 2)
-            RNS_LAUNCH_STREAM(2);
-        else
-            RNS_LAUNCH_STREAM(1);
+    if constexpr (MODE == kStashNone && RNS_STREAM_KS > 1) {
+        (void)ks;
+        RNS_LAUNCH_STREAM(RNS_STREAM_KS);
     } else {
-        (void)ks;  // receive verify: one set per wave (its stash is 5 chunks per datagram)
+        (void)ks;  // (receive verify: always one set per wave — its stash is 5 chunks per datagram)
         RNS_LAUNCH_STREAM(1);
     }
 #undef RNS_LAUNCH_STREAM
@@ -2379,8 +2588,13 @@ int launch_stream(const CsumArgs &a, int ks, hipStream_t st)
 int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
 {
     const bool nt = (sh.variant & 2u) != 0, buf = buf_records(a) < kOobOffset;
-    if (RNS_STREAM && a.align_mask >= 15u)  // 16-byte-aligned packets: the stream kernel
-        return launch_stream<kStashNone>(a, stream_sets(a.len_hint), st);
+    // 16-byte-aligned packets of a typical length above the tiny rounds kernel's and up to
+    // 1200 bytes (IMIX, 576-byte packets: profiles/r03_stream_ab.json) or unknown: the stream
+    // kernel.  MTU-sized packets keep the class kernel (c3: 238.5-239.8 vs 240.4-241.8 us per
+    // isolated dispatch), tiny ones the rounds kernel (c2: 13.2-13.7 vs 14.0-14.8 us).
+    const bool tiny = (sh.variant & ~16u) == 3u && sh.G == 4u && sh.U == 1u;
+    if (RNS_STREAM && a.align_mask >= 15u && !tiny && (a.len_hint == 0 || a.len_hint <= 1200))
+        return launch_stream<kStashNone>(a, 1, st);
     const uint64_t batches = (static_cast<uint64_t>(a.n) + 63) / 64;  // one wave per 64 packets
     const uint64_t wpb = ((sh.variant & 4u) ? kMixedBlock<false> : kBlock) / 64;  // waves per workgroup
     uint64_t blocks = (batches + wpb - 1) / wpb;
@@ -2656,6 +2870,22 @@ int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
     const bool nt = (frag_len_hint ? frag_len_hint : 512u) >= 384u;
 #endif
     const bool buf = buf_records(a) < kOobOffset;
+#ifndef RNS_CHAIN_STREAM  // A/B knob: 0 = the round-2 class-pass chain kernel
+#define RNS_CHAIN_STREAM 1
+#endif
+    if (RNS_CHAIN_STREAM) {  // fragments streamed 64 at a time as rows of chunks (RNS_FLAG_CHAIN_RUNS: no-op)
+        const dim3 sgrid(static_cast<uint32_t>(std::min<uint64_t>((static_cast<uint64_t>(n_pkts) + 63) / 64,
+                                                                  0x7FFFFFFFu))), sblock(64);
+        if (nt && buf)
+            hipLaunchKernelGGL((csum_chain_stream_kernel<true, true>), sgrid, sblock, 0, st, a);
+        else if (nt)
+            hipLaunchKernelGGL((csum_chain_stream_kernel<true, false>), sgrid, sblock, 0, st, a);
+        else if (buf)
+            hipLaunchKernelGGL((csum_chain_stream_kernel<false, true>), sgrid, sblock, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_chain_stream_kernel<false, false>), sgrid, sblock, 0, st, a);
+        return hip_status(hipGetLastError());
+    }
     // RNS_FLAG_CHAIN_RUNS: the run-checking kernel (buffer path; a hint, ignored otherwise)
     const bool runs = kChainRuns && (flags & RNS_FLAG_CHAIN_RUNS) && buf;
 #define RNS_CHAIN_LAUNCH(KM)                                                                      \

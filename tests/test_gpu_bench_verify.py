@@ -20,6 +20,14 @@ def test_bench_verify_rejects_exactly_the_corrupted(config, steps):
     assert v["rejected_total"] == v["rejected_expected"]
     assert v["datagrams_total"] > 0
     assert line["metric"] == bench.METRIC_VERIFY
-    assert line["roofline"]["kernel"].startswith("csum_mixed_kernel<RX>")
+    assert line["roofline"]["kernel"].startswith("csum_stream_kernel<RX>")
     assert 0 < line["roofline"]["frac"] < 1.0
     assert line["cpu_baseline"] is None
+
+
+def test_bench_verify_descriptor_form_matches():
+    """--desc 64 (rns_rx_verify_dev, the class kernel) rejects the same planted corruptions."""
+    line = bench.main(["--config", "c2_64B", "--op", "verify", "--desc", "64", "--steps", "12", "--warmup", "1",
+                       "--ramp-s", "0", "--traffic-json", "/nonexistent/{config}.json"])
+    assert line["roofline"]["kernel"].startswith("csum_mixed_kernel<RX>")
+    assert line["verify"]["rejected_total"] == line["verify"]["rejected_expected"] > 0
