@@ -60,10 +60,12 @@ def parse_args(argv=None):
                         "every packet is an IPv4/TCP datagram (checksums filled by rns_tx_fill_dev, every 1009th "
                         "corrupted) and a step is one rns_rx_verify_dev launch; at N>1 the SURVEY §8(e) leg is an "
                         "all-reduce(sum) of the per-rank rejected-datagram counts instead of the result all-gather")
-    p.add_argument("--desc", choices=("auto", "64", "32", "packed"), default="auto",
+    p.add_argument("--desc", choices=("auto", "64", "32", "packed", "strided"), default="auto",
                    help="descriptor form: 64 = u64 offsets (rns_csum_batch_dev); 32 = u32 offsets "
                         "(rns_csum_batch_dev_off32); packed = u16 lengths + one offset per 64 packets "
-                        "(rns_csum_batch_packed_dev); auto = packed, except for jumbo batches (the group "
+                        "(rns_csum_batch_packed_dev); strided = equal-length packets at a fixed stride, no "
+                        "offset or length descriptors (rns_csum_batch_strided_dev; fixed-size configs only); "
+                        "auto = strided for tiny equal-length packets (c2), packed otherwise, except for jumbo batches (the group "
                         "kernel, which has no 64-packet wave batches): 32 below 4 GiB, else 64")
     p.add_argument("--shape", default="", help="variant,G,U,max_blocks kernel shape override (tuning)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample duration (single thread)")
@@ -349,7 +351,11 @@ class GpuEngine:
         if form == "auto":
             small = self.layout.arena_bytes + 16 < 2 ** 32
             jumbo = self.layout.mean_len > 2500  # pick_shape's group kernel: no wave batches, no packed form
-            form = "64" if shape is not None else ("packed" if not jumbo else ("32" if small else "64"))
+            # tiny equal-length packets at a fixed stride (c2): the strided form, whose offsets need no
+            # descriptor load before a wave's first data load (isolated 13.68 -> 12.98 us, r03h)
+            tiny_fixed = op == "csum" and self.layout.mean_len < 128 and self.batches[0].stride() is not None
+            form = "64" if shape is not None else ("strided" if tiny_fixed else "packed" if not jumbo else
+                                                   ("32" if small else "64"))
         if op == "verify":  # packed receive arena (16-byte-aligned datagrams): the stream kernel; else 64-bit
             from rustnetworkstack_amd.workloads import make_verify_batch
             aligned = self.layout.n == 0 or int(self.layout.off[0]) % 16 == 0
@@ -361,10 +367,12 @@ class GpuEngine:
         self.form = form
         self.compact = form == "32"
         self.packed = form == "packed"
+        self.strided = form == "strided"
         self.verify_packed = op == "verify" and self.packed
         for b in self.batches:  # bind every rotating batch (and upload its descriptors) before any timing
             if op == "csum":
-                b.launcher(complement=True, shape=shape, compact=self.compact, packed=self.packed)
+                b.launcher(complement=True, shape=shape, compact=self.compact, packed=self.packed,
+                     strided=self.strided)
         self.k = 0
         self.used = set()  # indices of the rotating batches some step has run on
         self.last = self.batches[0]
@@ -395,7 +403,8 @@ class GpuEngine:
         if self.op == "verify":
             self._verify_call(b)()
         else:
-            b.launcher(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)()  # one ctypes call
+            b.launcher(complement=True, shape=self.shape, compact=self.compact, packed=self.packed,
+                     strided=self.strided)()  # one ctypes call
         self.last = b
 
     def capture(self, steps: int, streams: int = 1):
@@ -406,7 +415,8 @@ class GpuEngine:
         device: one kernel's ramp-up under the previous one's drain."""
         torch = self.torch
         if self.op == "csum":
-            fns = [b.rebind(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)
+            fns = [b.rebind(complement=True, shape=self.shape, compact=self.compact, packed=self.packed,
+                     strided=self.strided)
                    for b in self.batches]
             del fns  # (bound once outside the capture: descriptor uploads happen here, not inside it)
         side = [torch.cuda.Stream(device=self.device) for _ in range(max(streams, 1) - 1)]
@@ -425,7 +435,8 @@ class GpuEngine:
                     if self.op == "verify":
                         self._verify_call(b)()
                     else:
-                        b.rebind(complement=True, shape=self.shape, compact=self.compact, packed=self.packed)()
+                        b.rebind(complement=True, shape=self.shape, compact=self.compact, packed=self.packed,
+                     strided=self.strided)()
             for s_ in side:
                 cap.wait_stream(s_)
         self.sync()
@@ -732,6 +743,7 @@ def main(argv=None):
     algo_bytes = engine.payload_bytes + (1 if verify else 2) * engine.n
     # descriptor bytes a launch reads (seeds included): packed 2 B length + 8 B per 64 packets
     desc_bytes = (engine.n * (2 + (0 if verify else 2)) + 8 * ((engine.n + 63) // 64) if engine.packed
+                  else 2 * engine.n if getattr(engine, "strided", False)  # the seeds only
                   else engine.n * ((4 if engine.compact else 8) + 4 + (0 if verify else 2)))
     kernel_us = kernel_ms * 1e3
     achieved = algo_bytes / (kernel_us * 1e-6) / 1e9
@@ -772,7 +784,9 @@ def main(argv=None):
                             {"32": "u32 offset + u32 length + u16 seed (rns_csum_batch_dev_off32)",
                              "64": "u64 offset + u32 length + u16 seed (rns_csum_batch_dev)",
                              "packed": "packed: u16 length + u16 seed per packet, u64 offset per 64 packets "
-                                       "(rns_csum_batch_packed_dev)"})[engine.form],
+                                       "(rns_csum_batch_packed_dev)",
+                             "strided": "strided: u16 seed per packet; offsets and the one length implied "
+                                        "(rns_csum_batch_strided_dev)"})[engine.form],
             "rotating_batches": len(engine.batches),
             "rotation": ("one batch per graph stream at least, each with its own bytes: steps that may run at the same "
                          "time never read the same arena" if use_graph and args.graph_streams > 1 else

@@ -229,28 +229,62 @@ def csum_batch(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, see
                              shape=shape, compact=compact)()
 
 
+class StridedBatch:
+    """A device-resident batch of equal-length packets at a fixed stride
+    (rns_csum_batch_strided_dev), bound once like PreparedBatch: packet i =
+    arena[first_off + i*stride : + length].  No offset or length descriptors travel."""
+
+    def __init__(self, arena: torch.Tensor, n: int, stride: int, length: int, *, first_off: int = 0,
+                 seed: torch.Tensor | None = None, complement: bool = False,
+                 out: torch.Tensor | None = None, bad: torch.Tensor | None = None):
+        _require_cuda(arena, "arena", (torch.uint8,))
+        dev = arena.device
+        if n < 0 or n >= 2 ** 32 or stride < 0 or not 0 <= length < 2 ** 32 or first_off < 0:
+            raise ValueError("n, stride, length and first_off must be non-negative (n, length < 2^32)")
+        seed_ptr = None
+        if seed is not None:
+            _require_cuda(seed, "seed", _U16)
+            if seed.numel() != n or seed.device != dev:
+                raise ValueError("seed must have one entry per packet on the arena's device")
+            seed_ptr = seed.data_ptr()
+        if out is None:
+            out = torch.empty(n, dtype=torch.uint16, device=dev)
+        else:
+            _require_cuda(out, "out", _U16)
+            if out.numel() != n or out.device != dev:
+                raise ValueError("out must have one entry per packet on the arena's device")
+        bad_ptr = None
+        if bad is not None:
+            _require_cuda(bad, "bad", (torch.int32,))
+            bad_ptr = bad.data_ptr()
+        lib = _lib.load()
+        self._keep = (arena, seed, out, bad)
+        self.out, self.n, self.device = out, int(n), dev
+        self._fn = lib.rns_csum_batch_strided_dev
+        self._args = (arena.data_ptr(), arena.numel(), int(first_off), int(stride), int(length), seed_ptr,
+                      out.data_ptr(), int(n), _lib.RNS_FLAG_COMPLEMENT if complement else 0, bad_ptr,
+                      _stream_handle(dev))
+
+    def __call__(self) -> torch.Tensor:
+        if self.n:
+            if torch.cuda.current_device() != self.device.index:
+                with torch.cuda.device(self.device):
+                    st = self._fn(*self._args)
+            else:
+                st = self._fn(*self._args)
+            if st != _lib.RNS_OK:
+                raise _lib.ChecksumError(st, "rns_csum_batch_strided_dev")
+        return self.out
+
+
 def csum_batch_strided(arena: torch.Tensor, n: int, stride: int, length: int, *, first_off: int = 0,
                        seed: torch.Tensor | None = None, complement: bool = False,
                        out: torch.Tensor | None = None, bad: torch.Tensor | None = None) -> torch.Tensor:
     """Packets at a fixed stride: packet i = arena[first_off + i*stride : + length]."""
     _require_cuda(arena, "arena", (torch.uint8,))
-    dev = arena.device
-    seed_ptr = None
-    if seed is not None:
-        _require_cuda(seed, "seed", _U16)
-        if seed.numel() != n:
-            raise ValueError("seed must have one entry per packet")
-        seed_ptr = seed.data_ptr()
-    if out is None:
-        out = torch.empty(n, dtype=torch.uint16, device=dev)
-    bad_ptr = bad.data_ptr() if bad is not None else None
-    lib = _lib.load()
-    with torch.cuda.device(dev):
-        st = lib.rns_csum_batch_strided_dev(arena.data_ptr(), arena.numel(), first_off, stride, length, seed_ptr,
-                                            out.data_ptr(), n, _lib.RNS_FLAG_COMPLEMENT if complement else 0,
-                                            bad_ptr, _stream_handle(dev))
-    _lib.check(st, "rns_csum_batch_strided_dev")
-    return out
+    with torch.cuda.device(arena.device):
+        return StridedBatch(arena, n, stride, length, first_off=first_off, seed=seed, complement=complement,
+                            out=out, bad=bad)()
 
 
 def csum_chain(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch.Tensor, first: torch.Tensor,

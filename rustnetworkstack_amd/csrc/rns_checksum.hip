@@ -1954,6 +1954,9 @@ __device__ __forceinline__ uint4 keep_first(uint4 v, uint32_t c)
 #ifndef RNS_STREAM_RX_OCC  // waves/SIMD bound of the receive-verify instantiation (its finish needs registers)
 #define RNS_STREAM_RX_OCC 6
 #endif
+#ifndef RNS_STREAM_OUT  // A/B knob: result stores (0 plain, 1 nontemporal, 2 diagnostic: none)
+#define RNS_STREAM_OUT 1
+#endif
 constexpr int kStreamD = RNS_STREAM_D;
 
 // MODE kStashNone: the plain batch checksum (seed, optional complement, u16 out).
@@ -1987,18 +1990,67 @@ csum_stream_kernel(
         const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
     const uint64_t recs = buf_records(a);
     const uint64_t nunit = (static_cast<uint64_t>(a.n) + kNP - 1) / kNP;
+    // A wave that owns several units (capped grid: host knob RNS_STREAM_PERSIST) loads the next
+    // unit's descriptors while it streams this one, and stores a unit's results only after the
+    // NEXT unit's first rows are issued: gfx9 counts stores in vmcnt, in order, so a store issued
+    // before a load makes every wait for that load wait for the store's write acknowledgement
+    // too, and a one-shot wave holds its slot until its store completes.
+    const bool persist = gridDim.x < nunit;
+    uint32_t nx_len[KS], nx_seed[KS];
+    uint64_t nx_r0 = 0;
+    auto load_desc = [&](uint64_t uu) {  // branch-free: past the end re-reads the last unit
+        const uint64_t ub = uu < nunit ? uu : nunit - 1;
+        nx_r0 = a.blk_off[(ub * kNP) >> 6];
+#pragma unroll
+        for (int i = 0; i < KS; ++i) {
+            const uint64_t pp = ub * kNP + 64u * i + lane;
+            const uint64_t q = pp < a.n ? pp : a.n - 1;
+            nx_len[i] = pp < a.n ? static_cast<uint32_t>(a.len16[q]) : 0u;
+            nx_seed[i] = (!RX && a.seed && pp < a.n) ? static_cast<uint32_t>(a.seed[q]) : 0u;
+        }
+    };
+    load_desc(blockIdx.x);
+    uint32_t pend_res[KS];  // plain mode: the previous unit's results, not yet stored
+    uint64_t pend_base = ~0ull;
+#pragma unroll
+    for (int i = 0; i < KS; ++i)
+        pend_res[i] = 0;
+    auto store_results = [&](uint64_t b, const uint32_t *res) {
+#pragma unroll
+        for (int i = 0; i < KS; ++i) {
+            const uint64_t p = b + 64u * i + lane;
+            if (p < a.n) {
+#if RNS_STREAM_OUT == 1  // nontemporal result stores (IMIX isolated 472 -> 454 us, r03i)
+                __builtin_nontemporal_store(static_cast<uint16_t>(res[i]), a.out + p);
+#elif RNS_STREAM_OUT == 2  // diagnostic ONLY (results not written): the cost of the result stores
+                if (res[i] == 0xFFFFFFFFu)
+                    a.out[p] = 0;
+#else
+                a.out[p] = static_cast<uint16_t>(res[i]);  // 64 consecutive u16: one 128-byte store
+#endif
+            }
+        }
+    };
+    // after this unit's first rows are issued: the previous unit's stores, the next unit's descriptors
+    auto overlap_point = [&](uint64_t u_next) {
+        if constexpr (!RX) {
+            if (pend_base != ~0ull)
+                store_results(pend_base, pend_res);
+            pend_base = ~0ull;
+        }
+        if (persist)
+            load_desc(u_next);
+    };
 
     for (uint64_t u = blockIdx.x; u < nunit; u += gridDim.x) {
         const uint64_t base = u * kNP;
-        const uint64_t r0 = a.blk_off[base >> 6] + a.base_adjust;  // the wave's first packet
+        const uint64_t r0 = nx_r0 + a.base_adjust;  // the wave's first packet
         uint32_t len[KS], seed[KS], excl[KS];
         uint32_t total = 0;  // the region's bytes (a multiple of 16 on the stream path)
 #pragma unroll
         for (int i = 0; i < KS; ++i) {
-            const uint64_t p = base + 64u * i + lane;
-            const uint64_t q = p < a.n ? p : a.n - 1;  // branch-free: past the end re-reads the last
-            len[i] = p < a.n ? static_cast<uint32_t>(a.len16[q]) : 0u;
-            seed[i] = (!RX && a.seed && p < a.n) ? static_cast<uint32_t>(a.seed[q]) : 0u;
+            len[i] = nx_len[i];
+            seed[i] = nx_seed[i];
         }
 #pragma unroll
         for (int i = 0; i < KS; ++i) {
@@ -2039,6 +2091,8 @@ csum_stream_kernel(
                 issue(j, v[j]);
                 __builtin_amdgcn_sched_barrier(0);
             }
+            overlap_point(u + gridDim.x);
+            __builtin_amdgcn_sched_barrier(0);
             for (uint32_t k0 = 0; k0 < nrows; k0 += kStreamD) {
 #pragma unroll
                 for (int j = 0; j < kStreamD; ++j) {
@@ -2109,6 +2163,7 @@ csum_stream_kernel(
                 mine[i] = len[i] ? pend[64u * i + lane] - pstart[64u * i + lane] : 0u;
         } else {
             // ---- unaligned region (rare): the whole wave sums one packet at a time ----
+            overlap_point(u + gridDim.x);
 #pragma unroll
             for (int i = 0; i < KS; ++i) {
                 const uint64_t start = r0 + excl[i];
@@ -2157,9 +2212,7 @@ csum_stream_kernel(
                         a.l4_out[p] = static_cast<uint16_t>(l4_res);
                 }
             } else {
-                const uint16_t res = finalize_bits(mine[i], odd, false, seed[i], ok, a.flags);
-                if (live)
-                    a.out[p] = res;  // 64 consecutive u16: one 128-byte store
+                pend_res[i] = finalize_bits(mine[i], odd, false, seed[i], ok, a.flags);
                 if (a.bad) {
                     const uint64_t rejected = __ballot(live && !ok);
                     if (rejected && lane == 0)
@@ -2167,228 +2220,13 @@ csum_stream_kernel(
                 }
             }
         }
+        if constexpr (!RX)
+            pend_base = base;
         wave_lds_fence();  // the next range rewrites tab / pend / stash
     }
-}
-
-// ---------------------------------------------------------------------------
-// v5: fragment chains as a stream (util.rs:112-119 over NetBuffer fragments,
-// buf.rs:466-487).  A wave owns 64 consecutive packets; their fragments are taken 64
-// at a time (a SUB-BLOCK), and the sub-block's fragments are streamed as ONE sequence
-// of 16-byte chunks — fragment j's chunks, then fragment j+1's, wherever each lies in
-// the arena — in rows of 64 chunks, D rows in flight, so a 512-byte fragment is half a
-// row instead of a size-class unit of its own.  Per row a lane finds the fragment its
-// chunk belongs to with a max-scan of the fragments' start marks (fragments publish
-// their first virtual chunk), loads the chunk from that fragment's address, and zeroes
-// the bytes before the fragment start / after its end.  Prefix sums over the row give
-// each fragment's LE word sum (pend - pstart, exact for fragments <= 128 KiB), which is
-// folded and byte-swapped by the fragment's start parity (RFC 1071 §2(B)) into the
-// reference's per-fragment BE sum mod 0xffff; each packet's owner lane then folds its
-// fragments in order, exactly as util.rs:114-116 does.  A sub-block holding a fragment
-// longer than 128 KiB (the reference's u32 can wrap) sums its fragments one at a time
-// with the exact big-endian path instead.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v)
-{
-    uint32_t x = max(v, dpp_or_zero<0x111>(v));       // row_shr:1
-    x = max(x, dpp_or_zero<0x112>(v));                // row_shr:2
-    x = max(x, dpp_or_zero<0x113>(v));                // row_shr:3
-    x = max(x, dpp_or_zero<0x114, 0xF, 0xE>(x));      // row_shr:4, banks 1-3
-    x = max(x, dpp_or_zero<0x118, 0xF, 0xC>(x));      // row_shr:8, banks 2-3
-    x = max(x, dpp_or_zero<0x142, 0xA, 0xF>(x));      // row_bcast:15 into rows 1 and 3
-    x = max(x, dpp_or_zero<0x143, 0xC, 0xF>(x));      // row_bcast:31 into rows 2 and 3
-    return x;
-}
-
-#ifndef RNS_CHAIN_STREAM_OCC
-#define RNS_CHAIN_STREAM_OCC 6
-#endif
-
-template <bool NT, bool BUF>
-__global__ __launch_bounds__(64, RNS_CHAIN_STREAM_OCC) void csum_chain_stream_kernel(const CsumArgs a)
-{
-    __shared__ uint32_t mark[64];    // per row: the fragment (j+1, tagged) whose first chunk lane l loads
-    __shared__ uint4 finfo[64];      // per fragment of the sub-block: address, first virtual chunk, bounds
-    __shared__ uint32_t pend[64];    // per fragment: the prefix through its last chunk
-    __shared__ uint32_t pstart[64];  // per fragment: the prefix before its first chunk
-    const uint32_t lane = threadIdx.x;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
-    const uint64_t recs = buf_records(a);
-    constexpr uint32_t kBad = 0x80000000u;
-
-    for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * 64; base < a.n;
-         base += static_cast<uint64_t>(gridDim.x) * 64) {
-        const uint64_t p = base + lane;
-        const bool live = p < a.n;
-        uint32_t f0 = live ? a.first[p] : 0u, f1 = live ? a.first[p + 1] : 0u;
-        const bool rng_ok = f0 <= f1 && f1 <= a.n_frags;
-        if (!rng_ok)
-            f0 = f1 = 0;
-        uint32_t acc = ((a.seed && live) ? static_cast<uint32_t>(a.seed[p]) : 0u) | (rng_ok ? 0u : kBad);  // util.rs:113
-        const uint32_t F0 = wave_min_u32(f0 < f1 ? f0 : 0xFFFFFFFFu);
-        const uint32_t F1 = wave_max_u32(f0 < f1 ? f1 : 0u);
-        for (uint64_t fb = F0; fb < F1; fb += 64) {
-            const uint64_t f = fb + lane;
-            const bool has = f < F1;
-            const uint64_t foff = has ? a.off[f] + a.base_adjust : 0;
-            const uint32_t flen = has ? a.len[f] : 0u;
-            const bool fok = foff <= a.arena_bytes && flen <= a.arena_bytes - foff;
-            const uint32_t fs = static_cast<uint32_t>(foff & 15);
-            const bool big = fok && flen > kNoWrapBytes;
-            uint32_t g = 0;  // the fragment's folded BE sum (big: the exact BE sum mod 2^32)
-            if (!__ballot(big)) {
-                // ---- stream path ----
-                const uint32_t nch = (fok && flen) ? (fs + flen + 15) >> 4 : 0u;
-                const uint32_t vincl = wave_incl_scan(nch);
-                const uint32_t vex = vincl - nch;  // first virtual chunk
-                const uint32_t total = __builtin_amdgcn_readlane(vincl, 63);
-                const uint32_t nrows = (total + 63) >> 6;
-                finfo[lane] = make_uint4(static_cast<uint32_t>(foff & ~15ull), static_cast<uint32_t>(foff >> 32), vex,
-                                         fs | ((nch ? ((fs + flen - 1) & 15u) + 1u : 16u) << 8) | (nch << 13));
-                mark[lane] = 0xFFFFFFFFu;
-                wave_lds_fence();
-                uint32_t active = 0;  // j+1 of the fragment running at the end of the last looked-up row
-                uint32_t carry = 0;
-                // row k: which fragment each lane's chunk belongs to; its address and byte bounds
-                auto lookup = [&](uint32_t k, uint32_t &info) -> uint64_t {
-                    if (nch && (vex >> 6) == k)
-                        mark[vex & 63] = (k << 7) | (lane + 1);
-                    wave_lds_fence();
-                    const uint32_t m = mark[lane];
-                    const uint32_t jj = max(wave_incl_max((m >> 7) == k ? (m & 127u) : 0u), active);
-                    active = __builtin_amdgcn_readlane(jj, 63);
-                    const uint32_t v = (k << 6) + lane;
-                    const bool valid = jj != 0 && v < total;
-                    const uint4 fi = finfo[valid ? jj - 1 : 0];
-                    wave_lds_fence();
-                    const uint32_t rel = v - fi.z;
-                    const uint32_t lo = rel == 0 ? (fi.w & 15u) : 0u;
-                    const uint32_t last = (fi.w >> 13) - 1;
-                    const uint32_t hi = rel == last ? ((fi.w >> 8) & 31u) : 16u;
-                    info = valid ? 1u | ((jj - 1) << 1) | (lo << 7) | (hi << 11) | (rel == 0 ? 1u << 16 : 0u) |
-                                       (rel == last ? 1u << 17 : 0u)
-                                 : 0u;
-                    return valid ? ((static_cast<uint64_t>(fi.y) << 32) | fi.x) + (static_cast<uint64_t>(rel) << 4)
-                                 : recs;  // past the arena: no load
-                };
-                auto issue = [&](uint64_t off, uint4 &dst) {
-                    const bool in = off + 16 <= recs;
-                    if constexpr (BUF) {
-                        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(
-                            rsrc, in ? static_cast<uint32_t>(off) : kOobOffset, 0, NT ? kNtAux : 0);
-                        dst = make_uint4(x.x, x.y, x.z, x.w);
-                    } else {
-                        const uint4 x = load_chunk<NT>(a.arena + (in ? off : 0));
-                        dst = in ? x : make_uint4(0, 0, 0, 0);
-                    }
-                };
-                uint4 v[kStreamD];
-                uint32_t inf[kStreamD];
-#pragma unroll
-                for (int j = 0; j < kStreamD; ++j) {
-                    issue(lookup(j, inf[j]), v[j]);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                for (uint32_t k0 = 0; k0 < nrows; k0 += kStreamD) {
-#pragma unroll
-                    for (int j = 0; j < kStreamD; ++j) {
-                        const uint32_t k = k0 + j;
-                        const uint32_t in = inf[j];
-                        uint4 x = v[j];
-                        const uint32_t lo = (in >> 7) & 15u, hi = (in >> 11) & 31u;
-                        if (__ballot(lo != 0 || hi != 16)) {  // a fragment starts or ends inside a chunk here
-                            x.x = keep_bytes(x.x, static_cast<int>(lo), static_cast<int>(hi), 0);
-                            x.y = keep_bytes(x.y, static_cast<int>(lo), static_cast<int>(hi), 4);
-                            x.z = keep_bytes(x.z, static_cast<int>(lo), static_cast<int>(hi), 8);
-                            x.w = keep_bytes(x.w, static_cast<int>(lo), static_cast<int>(hi), 12);
-                        }
-                        uint32_t s = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
-                        s = __builtin_amdgcn_sad_u16(x.y, 0, s);
-                        s = __builtin_amdgcn_sad_u16(x.z, 0, s);
-                        s = __builtin_amdgcn_sad_u16(x.w, 0, s);
-                        s = (in & 1u) ? s : 0u;
-                        __builtin_amdgcn_sched_barrier(0);
-                        issue(lookup(k + kStreamD, inf[j]), v[j]);
-                        __builtin_amdgcn_sched_barrier(0);
-                        const uint32_t inc = wave_incl_scan(s);
-                        const uint32_t jl = (in >> 1) & 63u;
-                        if (in & (1u << 16))
-                            pstart[jl] = carry + inc - s;
-                        if (in & (1u << 17))
-                            pend[jl] = carry + inc;
-                        carry += __builtin_amdgcn_readlane(inc, 63);
-                        wave_lds_fence();
-                    }
-                }
-                const uint32_t w = nch ? pend[lane] - pstart[lane] : 0u;  // LE word sum, exact
-                const uint32_t x = fold16(w);
-                g = (foff & 1) ? x : (((x & 0xff) << 8) | (x >> 8));
-                wave_lds_fence();
-            } else {
-                // ---- a fragment past 128 KiB in this sub-block: one fragment at a time ----
-                uint64_t todo = __ballot(fok && flen != 0);
-                while (todo) {
-                    const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
-                    todo &= todo - 1;
-                    const uint64_t st =
-                        (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(foff >> 32), o)) << 32) |
-                        __builtin_amdgcn_readlane(static_cast<uint32_t>(foff), o);
-                    const uint32_t L = __builtin_amdgcn_readlane(flen, o);
-                    const Pkt k = make_pkt(st, L);
-                    uint32_t hs = 0, ls = 0, le = 0;
-                    for (uint32_t cc = 0; cc < k.nch; cc += 64) {
-                        uint4 wv[1];
-                        issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, wv);
-                        mask_edges<64, 1, 1>(k, cc + lane, wv);
-                        if (k.big)
-                            sum_be<1, 1>(wv, (st & 1) ? 0x01000100u : 0x00010001u, hs, ls);
-                        else
-                            le = sum_le<1, 1>(wv, le);
-                    }
-                    const uint32_t sum = group_allreduce<64>(k.big ? (hs << 8) + ls : le);
-                    uint32_t gv = sum;
-                    if (!k.big) {
-                        const uint32_t xx = fold16(sum);
-                        gv = (st & 1) ? xx : (((xx & 0xff) << 8) | (xx >> 8));
-                    }
-                    g = lane == o ? gv : g;
-                }
-            }
-            // owner lanes: each packet's fragments inside [fb, fb + 64), in order (util.rs:114-116)
-            const uint32_t gflag = (big ? 1u : 0u) | ((has && !fok) ? 2u : 0u);
-            uint64_t t = max(static_cast<uint64_t>(f0), fb);
-            const uint64_t hi = min(static_cast<uint64_t>(f1), fb + 64);
-            while (__ballot(t < hi)) {
-                const bool act = t < hi;
-                const int src = act ? static_cast<int>(t - fb) : 0;
-                const uint32_t gv = static_cast<uint32_t>(__shfl(static_cast<int>(g), src, 64));
-                const uint32_t fv = static_cast<uint32_t>(__shfl(static_cast<int>(gflag), src, 64));
-                if (act) {
-                    const uint32_t bad = (acc & kBad) | ((fv & 2u) ? kBad : 0u);
-                    uint32_t s = (acc & 0xffffu) + gv;  // big: util.rs:89-99 mod 2^32; else <= 0x1fffe
-                    if (fv & 1u) {
-                        while (s > 0xffff)  // util.rs:101-103
-                            s = (s & 0xffff) + (s >> 16);
-                    } else {
-                        s = (s & 0xffff) + (s >> 16);  // one end-around step folds it
-                    }
-                    acc = s | bad;
-                    ++t;
-                }
-            }
-        }
-        uint32_t r = acc & 0xffffu;
-        if (a.flags & RNS_FLAG_COMPLEMENT)
-            r ^= 0xffff;
-        const bool ok = !(acc & kBad);
-        if (live)
-            a.out[p] = static_cast<uint16_t>(ok ? r : 0u);  // 64 consecutive u16: one 128-byte store
-        if (a.bad) {
-            const uint64_t rejected = __ballot(live && !ok);
-            if (rejected && lane == 0)
-                atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
-        }
+    if constexpr (!RX) {
+        if (pend_base != ~0ull)
+            store_results(pend_base, pend_res);
     }
 }
 
@@ -2560,11 +2398,37 @@ Shape pick_shape(uint32_t len_hint)
 #ifndef RNS_STREAM_KS  // A/B knob: packet sets per wave
 #define RNS_STREAM_KS 1
 #endif
+// Compute units of the current device (256 on MI355X), cached per device.
+int device_cus()
+{
+    static int cus[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+        return 256;
+    if (cus[dev] == 0) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+            c = 256;
+        cus[dev] = c;
+    }
+    return cus[dev];
+}
+
 template <int MODE>
 int launch_stream(const CsumArgs &a, int ks, hipStream_t st)
 {
     const bool buf = buf_records(a) < kOobOffset;
-    const uint64_t units = (static_cast<uint64_t>(a.n) + 64u * ks - 1) / (64u * ks);
+    uint64_t units = (static_cast<uint64_t>(a.n) + 64u * ks - 1) / (64u * ks);
+#ifndef RNS_STREAM_TINY_CAP  // A/B knob: grid cap (waves loop over units) for ACK-sized packets; 0 = none
+#define RNS_STREAM_TINY_CAP 0
+#endif
+#ifndef RNS_STREAM_PERSIST  // A/B knob: at most this many waves per SIMD (waves loop over units); 0 = none
+#define RNS_STREAM_PERSIST 0
+#endif
+    if (RNS_STREAM_TINY_CAP && a.arena_bytes / std::max<uint64_t>(a.n, 1) <= 128)
+        units = std::min<uint64_t>(units, RNS_STREAM_TINY_CAP);
+    if (RNS_STREAM_PERSIST)
+        units = std::min<uint64_t>(units, static_cast<uint64_t>(device_cus()) * 4u * RNS_STREAM_PERSIST);
     const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(units, 0x7FFFFFFFu))), block(64);
     constexpr bool NT = RNS_STREAM_NT != 0;
 #define RNS_LAUNCH_STREAM(K)                                                                       \
@@ -2870,22 +2734,6 @@ int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
     const bool nt = (frag_len_hint ? frag_len_hint : 512u) >= 384u;
 #endif
     const bool buf = buf_records(a) < kOobOffset;
-#ifndef RNS_CHAIN_STREAM  // A/B knob: 0 = the round-2 class-pass chain kernel
-#define RNS_CHAIN_STREAM 1
-#endif
-    if (RNS_CHAIN_STREAM) {  // fragments streamed 64 at a time as rows of chunks (RNS_FLAG_CHAIN_RUNS: no-op)
-        const dim3 sgrid(static_cast<uint32_t>(std::min<uint64_t>((static_cast<uint64_t>(n_pkts) + 63) / 64,
-                                                                  0x7FFFFFFFu))), sblock(64);
-        if (nt && buf)
-            hipLaunchKernelGGL((csum_chain_stream_kernel<true, true>), sgrid, sblock, 0, st, a);
-        else if (nt)
-            hipLaunchKernelGGL((csum_chain_stream_kernel<true, false>), sgrid, sblock, 0, st, a);
-        else if (buf)
-            hipLaunchKernelGGL((csum_chain_stream_kernel<false, true>), sgrid, sblock, 0, st, a);
-        else
-            hipLaunchKernelGGL((csum_chain_stream_kernel<false, false>), sgrid, sblock, 0, st, a);
-        return hip_status(hipGetLastError());
-    }
     // RNS_FLAG_CHAIN_RUNS: the run-checking kernel (buffer path; a hint, ignored otherwise)
     const bool runs = kChainRuns && (flags & RNS_FLAG_CHAIN_RUNS) && buf;
 #define RNS_CHAIN_LAUNCH(KM)                                                                      \

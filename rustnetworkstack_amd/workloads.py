@@ -131,16 +131,39 @@ class DeviceBatch:
         self.out = torch.empty(layout.n, dtype=torch.uint16, device=self.device)
         self._prepared = {}
 
-    def launcher(self, complement: bool = False, shape=None, compact: bool = False, packed: bool = False):
+    def stride(self):
+        """(first_off, stride, length) if every packet has one length and the packets lie at
+        a fixed stride (c2-c4: fixed-size configs), else None."""
+        lay = self.layout
+        if lay.n == 0 or not np.all(lay.length == lay.length[0]):
+            return None
+        step = int(lay.off[1] - lay.off[0]) if lay.n > 1 else ALIGN
+        if lay.n > 1 and not np.array_equal(np.diff(lay.off), np.full(lay.n - 1, step, dtype=np.uint64)):
+            return None
+        return int(lay.off[0]), step, int(lay.length[0])
+
+    def launcher(self, complement: bool = False, shape=None, compact: bool = False, packed: bool = False,
+                 strided: bool = False):
         """Pre-bound launch (one ctypes call per launch) on the current stream.
         ``compact`` binds 32-bit offsets (rns_csum_batch_dev_off32; arenas < 4 GiB);
         ``packed`` binds the packed form (rns_csum_batch_packed_dev: u16 lengths + one
-        offset per 64 packets; the synthetic layouts ARE packed at 16-byte alignment)."""
+        offset per 64 packets; the synthetic layouts ARE packed at 16-byte alignment);
+        ``strided`` binds the fixed-stride form (rns_csum_batch_strided_dev: equal-length
+        packets, no offset or length descriptors)."""
         import torch
 
-        from .batch import PackedBatch, PreparedBatch, packed_layout
-        key = (complement, shape, compact, packed)
+        from .batch import PackedBatch, PreparedBatch, StridedBatch, packed_layout
+        key = (complement, shape, compact, packed, strided)
         if key not in self._prepared:
+            if strided:
+                if shape is not None or compact or packed:
+                    raise ValueError("the strided form takes no shape override, compact or packed descriptors")
+                st = self.stride()
+                if st is None:
+                    raise ValueError("layout is not equal-length packets at a fixed stride")
+                self._prepared[key] = StridedBatch(self.arena, self.layout.n, st[1], st[2], first_off=st[0],
+                                                   seed=self.seed, complement=complement, out=self.out)
+                return self._prepared[key]
             if packed:
                 if shape is not None or compact:
                     raise ValueError("the packed form takes no shape override and no compact offsets")
@@ -164,12 +187,17 @@ class DeviceBatch:
                                                 compact=compact)
         return self._prepared[key]
 
-    def rebind(self, complement: bool = False, shape=None, compact: bool = False, packed: bool = False):
+    def rebind(self, complement: bool = False, shape=None, compact: bool = False, packed: bool = False,
+               strided: bool = False):
         """A fresh launcher bound to the CURRENT stream (e.g. a graph-capture stream),
         from the descriptors launcher() already uploaded (no copies: safe inside a
         capture).  Not cached."""
-        from .batch import PackedBatch, PreparedBatch
-        bound = self.launcher(complement, shape, compact, packed)  # uploads once, outside any capture
+        from .batch import PackedBatch, PreparedBatch, StridedBatch
+        bound = self.launcher(complement, shape, compact, packed, strided)  # uploads once, outside any capture
+        if strided:
+            st = self.stride()
+            return StridedBatch(self.arena, self.layout.n, st[1], st[2], first_off=st[0], seed=self.seed,
+                                complement=complement, out=self.out)
         if packed:
             return PackedBatch(self.arena, self.blk_off, self.len16, self.seed, align_log2=ALIGN.bit_length() - 1,
                                complement=complement, out=self.out, len_hint=int(round(self.layout.mean_len)))

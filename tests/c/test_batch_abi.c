@@ -128,6 +128,45 @@ static int test_packed(hipStream_t st)
     return 0;
 }
 
+/* rns_csum_batch_strided_dev (util.rs:88-110 per packet, fixed-size slots): 64-byte packets
+ * at a 64-byte stride (the bench's c2 form) and 40-byte packets at an odd start and stride. */
+static int test_strided(hipStream_t st)
+{
+    const uint32_t n = 64 * 500 + 3;
+    const struct { uint64_t first, stride; uint32_t len; } cases[2] = {{0, 64, 64}, {7, 41, 40}};
+    uint16_t *seed = malloc(n * sizeof *seed), *want = malloc(n * sizeof *want), *got = malloc(n * sizeof *got);
+    for (uint32_t i = 0; i < n; ++i)
+        seed[i] = (uint16_t)next_u64();
+    for (int c = 0; c < 2; ++c) {
+        const uint64_t bytes = cases[c].first + (uint64_t)cases[c].stride * n + 16;
+        uint8_t *arena = malloc(bytes);
+        fill_random(arena, bytes);
+        for (uint32_t i = 0; i < n; ++i)
+            want[i] = (uint16_t)(0xffffu ^ (uint32_t)oracle_compute_ones_comp(
+                                               seed[i], arena + cases[c].first + (uint64_t)i * cases[c].stride,
+                                               cases[c].len));
+        uint8_t *d_arena;
+        uint16_t *d_seed, *d_out;
+        HIP_OK(hipMalloc((void **)&d_arena, bytes));
+        HIP_OK(hipMalloc((void **)&d_seed, n * sizeof *seed));
+        HIP_OK(hipMalloc((void **)&d_out, n * sizeof *got));
+        HIP_OK(hipMemcpy(d_arena, arena, bytes, hipMemcpyHostToDevice));
+        HIP_OK(hipMemcpy(d_seed, seed, n * sizeof *seed, hipMemcpyHostToDevice));
+        HIP_OK(hipMemset(d_out, 0, n * sizeof *got));
+        CHECK(rns_csum_batch_strided_dev(d_arena, bytes, cases[c].first, cases[c].stride, cases[c].len, d_seed, d_out,
+                                         n, RNS_FLAG_COMPLEMENT, NULL, st) == RNS_OK,
+              "rns_csum_batch_strided_dev case %d", c);
+        HIP_OK(hipStreamSynchronize(st));
+        HIP_OK(hipMemcpy(got, d_out, n * sizeof *got, hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < n; ++i)
+            CHECK(got[i] == want[i], "strided case %d packet %u: %04x != %04x", c, i, got[i], want[i]);
+        hipFree(d_arena); hipFree(d_seed); hipFree(d_out);
+        free(arena);
+    }
+    free(seed); free(want); free(got);
+    return 0;
+}
+
 /* rns_csum_chain_dev (util.rs:112-119 over NetBuffer fragments, buf.rs:466-487): packets of
  * 0..6 fragments of 1..700 bytes at scattered offsets, odd non-final fragments included,
  * with and without the runs hint; half the packets' fragments are adjacent views. */
@@ -397,7 +436,7 @@ int main(void)
 
     /* 2b. the packed entry bench.py times, the fragment-chain entry, transmit finalize and
      *     receive verify: each against the oracle's util.rs restatement */
-    if (test_packed(st) || test_chains(st) || test_tx_rx(st))
+    if (test_packed(st) || test_strided(st) || test_chains(st) || test_tx_rx(st))
         return 2;
 
     /* 3. errors come back as status codes, never as aborts */

@@ -46,3 +46,13 @@ def test_every_graph_stream_reads_its_own_batch():
     g.replay()
     torch.cuda.synchronize()
     assert eng.used == {0, 1, 2}
+
+
+def test_bench_c2_strided_form():
+    """--desc strided (rns_csum_batch_strided_dev: no offset/length descriptors) on the c2
+    config: the CPU-baseline leg re-checks the rotating batches' results against the oracle."""
+    line = bench.main(["--config", "c2_64B", "--desc", "strided", "--steps", "24", "--warmup", "1", "--ramp-s", "0",
+                       "--cpu-seconds", "1", "--no-host-pipeline", "--traffic-json", "/nonexistent/{config}.json"])
+    assert line["config"]["descriptors"].startswith("strided")
+    assert line["roofline"]["descriptor_bytes_per_launch"] == 2 * (1 << 20)
+    assert line["cpu_baseline"]["gpu_sample_bit_exact"] is True

@@ -286,3 +286,17 @@ def test_packets_ending_at_unpadded_arena_end(oracle, total):
     for shape in [None] + [(v, g, u, 0) for v in range(8) for g, u in ((4, 1), (16, 4), (64, 2))] + \
             [(9, 4, 1, 0), (11, 2, 2, 0), (11, 8, 1, 3)]:
         assert np.array_equal(host_u16(csum_batch(arena, *d, shape=shape)), expect), shape
+
+
+@pytest.mark.parametrize("name", ["c2_64B", "c3_1500B"])
+def test_strided_form_full_size_bit_exact(oracle, name):
+    """The fixed-stride form bench.py --desc strided binds (DeviceBatch.launcher(strided=True)),
+    every packet of the full config against the C oracle."""
+    lay = make_layout(name)
+    b = DeviceBatch(lay, DEV)
+    assert b.stride() == (0, int(lay.off[1]), int(lay.length[0]))
+    b.launcher(complement=True, strided=True)()
+    got = b.host_out()
+    expect = oracle.batch(b.host_arena(), lay.off, lay.length, lay.seed, complement=True, threads=16)
+    assert np.array_equal(got, expect)
+    del b

@@ -64,3 +64,16 @@ def test_packed_layout_matches_synthetic_offsets():
         expect = 9 + np.concatenate([[0], np.cumsum((ln + m) & ~m)])
         assert np.array_equal(off, expect[:-1]) and end == int(expect[-1])
         assert np.array_equal(blk, off[::64])
+
+
+def test_device_batch_stride_detection():
+    """DeviceBatch.stride() (bench.py --desc strided): fixed-size configs are equal-length
+    packets at a fixed stride; IMIX is not (no device needed: the check reads the layout)."""
+    from rustnetworkstack_amd.workloads import DeviceBatch
+    b = object.__new__(DeviceBatch)
+    b.layout = W.make_layout("c2_64B", n=1000)
+    assert b.stride() == (0, 64, 64)
+    b.layout = W.make_layout("c3_1500B", n=1000)
+    assert b.stride() == (0, 1504, 1500)
+    b.layout = W.make_layout("c5_imix", n=1000)
+    assert b.stride() is None
