@@ -711,8 +711,15 @@ __global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
                 v[u] = w[u];
         }
         const uint16_t acc = finalize(mine, d_start, d_len, d_seed, d_ok, a.flags);
-        if (live)
-            a.out[p] = static_cast<uint16_t>(acc);  // 64 consecutive u16: one 128-byte store
+#ifndef RNS_ROUNDS_NTSTORE  // A/B knob: nontemporal result stores in the rounds kernel
+#define RNS_ROUNDS_NTSTORE 0
+#endif
+        if (live) {
+            if constexpr (RNS_ROUNDS_NTSTORE != 0)
+                __builtin_nontemporal_store(static_cast<uint16_t>(acc), a.out + p);
+            else
+                a.out[p] = static_cast<uint16_t>(acc);  // 64 consecutive u16: one 128-byte store
+        }
         if (a.bad) {
             const uint64_t rejected = __ballot(live && !d_ok);
             if (rejected && lane == 0)
@@ -1625,8 +1632,15 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX
             res = d_ok ? static_cast<uint16_t>(mine) : static_cast<uint16_t>(0);  // finished (and stored) in-round
         else
             res = finalize_bits(mine, odd, big, d_seed, d_ok, a.flags);
-        if (live && a.out)
-            a.out[p] = res;  // 64 consecutive u16: one 128-byte store
+#ifndef RNS_MIXED_NTSTORE  // A/B knob: nontemporal result stores in the plain class kernel
+#define RNS_MIXED_NTSTORE 0
+#endif
+        if (live && a.out) {
+            if constexpr (RNS_MIXED_NTSTORE != 0 && !FILL && !RX && !TX)
+                __builtin_nontemporal_store(res, a.out + p);
+            else
+                a.out[p] = res;  // 64 consecutive u16: one 128-byte store
+        }
         if constexpr (FILL && !kFillInRound) {
             if (live && d_ok)  // set_be16(&mut header[f..f+2], checksum), after the wave read its 64 packets
                 fill_store(a, fs, d_start, d_field, res, st + pos * kNS);
@@ -1968,13 +1982,20 @@ constexpr int kStreamD = RNS_STREAM_D;
 // as one row sequence: small packets (IMIX, ACKs) give a wave KS times the bytes, so the
 // per-wave start (descriptor load, first row latency) and end are paid KS times less
 // often.  Lane l owns packets 64*i + l of the wave's range (i < KS).
-template <int MODE, int KS, bool NT, bool BUF>
+// XO (capped grid, plain mode, buffer path): every row step issues exactly one extra memory
+// operation after its row load — the previous unit's result store, one of the next unit's
+// three descriptor loads, or an out-of-range (dropped) buffer store — so the vmcnt pattern
+// is the same for every row of every unit and the compiler's counted waits stay exact
+// (vmcnt(2D-1)); extra operations issued only at a unit's start would merge into the loop's
+// steady state as a wait for all D rows in flight.
+template <int MODE, int KS, bool NT, bool BUF, bool XO = false>
 __global__ __launch_bounds__(64, MODE == kStashHead ? RNS_STREAM_RX_OCC : KS == 4 ? 5 : RNS_STREAM_OCC) void
 csum_stream_kernel(
     const CsumArgs a)
 {
     static_assert(MODE == kStashNone || MODE == kStashHead, "stream modes: plain, receive verify");
     static_assert(KS == 1 || KS == 2 || KS == 4, "packet sets per wave");
+    static_assert(!XO || (MODE == kStashNone && KS == 1 && BUF && kStreamD >= 4), "XO: plain mode, one set, buffers");
     constexpr bool RX = MODE == kStashHead;
     constexpr int kNS = RX ? 5 : 1;  // stash chunks per datagram (the unaligned path fills 5)
     constexpr uint32_t kNP = 64u * KS;
@@ -1998,9 +2019,12 @@ csum_stream_kernel(
     const bool persist = gridDim.x < nunit;
     uint32_t nx_len[KS], nx_seed[KS];
     uint64_t nx_r0 = 0;
+    // (the block offset is loaded per lane at an index the compiler cannot prove uniform: a
+    // uniform load is moved to SGPRs right away, with a vmcnt(0) wait for every row in flight)
+    const uint32_t zero_v = __builtin_amdgcn_mbcnt_lo(0u, 0u);
     auto load_desc = [&](uint64_t uu) {  // branch-free: past the end re-reads the last unit
         const uint64_t ub = uu < nunit ? uu : nunit - 1;
-        nx_r0 = a.blk_off[(ub * kNP) >> 6];
+        nx_r0 = a.blk_off[((ub * kNP) >> 6) + zero_v];
 #pragma unroll
         for (int i = 0; i < KS; ++i) {
             const uint64_t pp = ub * kNP + 64u * i + lane;
@@ -2041,16 +2065,52 @@ csum_stream_kernel(
         if (persist)
             load_desc(u_next);
     };
+    // XO: the results as buffer stores (out-of-range offset: dropped by the hardware, no traffic)
+    const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        a.out, static_cast<short>(0), static_cast<int>(XO ? 2u * a.n : 0u), 0x00020000);
+    auto xo_store = [&](bool real) {
+        const uint64_t p = pend_base + lane;
+        const bool ok = real && pend_base != ~0ull && p < a.n;
+        __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(pend_res[0]), out_rsrc,
+                                              ok ? static_cast<uint32_t>(2 * p) : kOobOffset, 0,
+                                              RNS_STREAM_OUT == 1 ? kNtAux : 0);
+        if (real)
+            pend_base = ~0ull;
+    };
+    // XO: extra operation j of the first row block (j < 4), a dropped store otherwise
+    auto xo_op = [&](int j, bool first_block, uint64_t u_next) {
+        const uint64_t ub = u_next < nunit ? u_next : nunit - 1;
+        const uint64_t pp = ub * kNP + lane;
+        const uint64_t q = pp < a.n ? pp : a.n - 1;
+        if (!first_block || j > 3) {
+            xo_store(false);
+        } else if (j == 0) {
+            xo_store(true);
+        } else if (j == 1) {
+            nx_r0 = a.blk_off[((ub * kNP) >> 6) + zero_v];
+        } else if (j == 2) {
+            nx_len[0] = static_cast<uint32_t>(a.len16[q]);  // (zeroed past the end at the unit's start)
+        } else {
+            if (a.seed)
+                nx_seed[0] = static_cast<uint32_t>(a.seed[q]);
+            else
+                xo_store(false);
+        }
+    };
 
     for (uint64_t u = blockIdx.x; u < nunit; u += gridDim.x) {
         const uint64_t base = u * kNP;
-        const uint64_t r0 = nx_r0 + a.base_adjust;  // the wave's first packet
+        const uint64_t r0 = ((static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nx_r0 >> 32)))
+                              << 32) |
+                             __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nx_r0))) +
+                            a.base_adjust;  // the wave's first packet
         uint32_t len[KS], seed[KS], excl[KS];
         uint32_t total = 0;  // the region's bytes (a multiple of 16 on the stream path)
 #pragma unroll
         for (int i = 0; i < KS; ++i) {
-            len[i] = nx_len[i];
-            seed[i] = nx_seed[i];
+            const bool in = base + 64u * i + lane < a.n;
+            len[i] = (!XO || in) ? nx_len[i] : 0u;
+            seed[i] = (!XO || (in && a.seed)) ? nx_seed[i] : 0u;
         }
 #pragma unroll
         for (int i = 0; i < KS; ++i) {
@@ -2090,9 +2150,15 @@ csum_stream_kernel(
             for (int j = 0; j < kStreamD; ++j) {
                 issue(j, v[j]);
                 __builtin_amdgcn_sched_barrier(0);
+                if constexpr (XO) {
+                    xo_store(false);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             }
-            overlap_point(u + gridDim.x);
-            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (!XO) {
+                overlap_point(u + gridDim.x);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             for (uint32_t k0 = 0; k0 < nrows; k0 += kStreamD) {
 #pragma unroll
                 for (int j = 0; j < kStreamD; ++j) {
@@ -2147,6 +2213,10 @@ csum_stream_kernel(
                     __builtin_amdgcn_sched_barrier(0);
                     issue(k + kStreamD, v[j]);
                     __builtin_amdgcn_sched_barrier(0);
+                    if constexpr (XO) {
+                        xo_op(j, k0 == 0, u + gridDim.x);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
                     const uint32_t inc = wave_incl_scan(s);
                     if (mark && (t & kStart))
                         pstart[pk] = carry + inc - s;
@@ -2156,6 +2226,13 @@ csum_stream_kernel(
                     wave_lds_fence();
                 }
             }
+            if constexpr (XO) {
+                if (nrows == 0) {  // no row steps: the extra operations now
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        xo_op(j, true, u + gridDim.x);
+                }
+            }
             // a packet's sum: the region prefix through its last chunk minus the prefix before its
             // first (u32 differences: exact, a packet's LE sum is < 2^32)
 #pragma unroll
@@ -2163,7 +2240,13 @@ csum_stream_kernel(
                 mine[i] = len[i] ? pend[64u * i + lane] - pstart[64u * i + lane] : 0u;
         } else {
             // ---- unaligned region (rare): the whole wave sums one packet at a time ----
-            overlap_point(u + gridDim.x);
+            if constexpr (XO) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    xo_op(j, true, u + gridDim.x);
+            } else {
+                overlap_point(u + gridDim.x);
+            }
 #pragma unroll
             for (int i = 0; i < KS; ++i) {
                 const uint64_t start = r0 + excl[i];
@@ -2206,8 +2289,14 @@ csum_stream_kernel(
                 const uint8_t stv = rx_finish<kNS>(a, stash + (64u * i + lane) * kNS, mine[i],
                                                    static_cast<uint32_t>(start & 15), len[i], odd, false,
                                                    live && ok && len[i] != 0, l4_res);
+#ifndef RNS_STREAM_RX_NTSTORE  // A/B knob: nontemporal status stores in the stream receive verify
+#define RNS_STREAM_RX_NTSTORE 0
+#endif
                 if (live) {
-                    a.status[p] = stv;
+                    if constexpr (RNS_STREAM_RX_NTSTORE != 0)
+                        __builtin_nontemporal_store(stv, a.status + p);
+                    else
+                        a.status[p] = stv;
                     if (a.l4_out)
                         a.l4_out[p] = static_cast<uint16_t>(l4_res);
                 }
@@ -2224,7 +2313,9 @@ csum_stream_kernel(
             pend_base = base;
         wave_lds_fence();  // the next range rewrites tab / pend / stash
     }
-    if constexpr (!RX) {
+    if constexpr (XO) {
+        xo_store(true);
+    } else if constexpr (!RX) {
         if (pend_base != ~0ull)
             store_results(pend_base, pend_res);
     }
@@ -2418,12 +2509,16 @@ template <int MODE>
 int launch_stream(const CsumArgs &a, int ks, hipStream_t st)
 {
     const bool buf = buf_records(a) < kOobOffset;
-    uint64_t units = (static_cast<uint64_t>(a.n) + 64u * ks - 1) / (64u * ks);
+    const uint64_t all_units = (static_cast<uint64_t>(a.n) + 64u * ks - 1) / (64u * ks);
+    uint64_t units = all_units;
 #ifndef RNS_STREAM_TINY_CAP  // A/B knob: grid cap (waves loop over units) for ACK-sized packets; 0 = none
 #define RNS_STREAM_TINY_CAP 0
 #endif
 #ifndef RNS_STREAM_PERSIST  // A/B knob: at most this many waves per SIMD (waves loop over units); 0 = none
 #define RNS_STREAM_PERSIST 0
+#endif
+#ifndef RNS_STREAM_XO  // A/B knob: capped grids run the extra-operation-per-row form (plain mode)
+#define RNS_STREAM_XO 1
 #endif
     if (RNS_STREAM_TINY_CAP && a.arena_bytes / std::max<uint64_t>(a.n, 1) <= 128)
         units = std::min<uint64_t>(units, RNS_STREAM_TINY_CAP);
@@ -2441,6 +2536,10 @@ int launch_stream(const CsumArgs &a, int ks, hipStream_t st)
     if constexpr (MODE == kStashNone && RNS_STREAM_KS > 1) {
         (void)ks;
         RNS_LAUNCH_STREAM(RNS_STREAM_KS);
+    } else if (MODE == kStashNone && RNS_STREAM_XO && buf && grid.x < all_units && a.n < (1u << 31)) {
+        // a capped grid on the buffer path: the extra-operation-per-row form (delayed stores,
+        // next unit's descriptors in flight)
+        hipLaunchKernelGGL((csum_stream_kernel<kStashNone, 1, NT, true, true>), grid, block, 0, st, a);
     } else {
         (void)ks;  // (receive verify: always one set per wave — its stash is 5 chunks per datagram)
         RNS_LAUNCH_STREAM(1);
@@ -2457,7 +2556,10 @@ int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
     // kernel.  MTU-sized packets keep the class kernel (c3: 238.5-239.8 vs 240.4-241.8 us per
     // isolated dispatch), tiny ones the rounds kernel (c2: 13.2-13.7 vs 14.0-14.8 us).
     const bool tiny = (sh.variant & ~16u) == 3u && sh.G == 4u && sh.U == 1u;
-    if (RNS_STREAM && a.align_mask >= 15u && !tiny && (a.len_hint == 0 || a.len_hint <= 1200))
+#ifndef RNS_STREAM_MAXLEN  // A/B knob: the stream kernel for typical lengths up to this
+#define RNS_STREAM_MAXLEN 1200
+#endif
+    if (RNS_STREAM && a.align_mask >= 15u && !tiny && (a.len_hint == 0 || a.len_hint <= RNS_STREAM_MAXLEN))
         return launch_stream<kStashNone>(a, 1, st);
     const uint64_t batches = (static_cast<uint64_t>(a.n) + 63) / 64;  // one wave per 64 packets
     const uint64_t wpb = ((sh.variant & 4u) ? kMixedBlock<false> : kBlock) / 64;  // waves per workgroup

@@ -1,0 +1,22 @@
+B="--no-cpu-baseline --no-host-pipeline --steps 20 --warmup 5"
+A=$GRAFT_REPO_ROOT/tools/ab/librns_checksum_
+steps=(pytest 900 "python -u -m pytest tests -m gpu -q -p no:cacheprovider --maxfail 5 --timeout 300 --timeout-method thread"
+       smoke 200 "python -c 'import __graft_entry__ as g; g.smoke()'")
+for v in p8 p6 p4 p8o0; do
+  steps+=(py_$v 300 "RNS_CHECKSUM_LIB=$A$v.so python -u -m pytest tests/test_gpu_packed.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread")
+done
+for cfg in c5_imix d576B d1000B; do
+  for v in main p8 p6 p4 p8o0; do
+    if [ $v = main ]; then E=""; else E="RNS_CHECKSUM_LIB=$A$v.so"; fi
+    steps+=(${cfg}_$v 200 "$E python bench.py $B --config $cfg")
+  done
+done
+for v in main p8; do
+  if [ $v = main ]; then E=""; else E="RNS_CHECKSUM_LIB=$A$v.so"; fi
+  steps+=(sh0_$v 200 "$E python bench.py $B --config c5_imix --shard 0/8")
+done
+for v in main tcap4k tcap2k; do
+  if [ $v = main ]; then E=""; else E="RNS_CHECKSUM_LIB=$A$v.so"; fi
+  steps+=(v_c2_$v 200 "$E python bench.py $B --config c2_64B --op verify --steps 200")
+done
+bash tools/gpu_steps.sh r03k "${steps[@]}"
