@@ -1968,6 +1968,9 @@ __device__ __forceinline__ uint4 keep_first(uint4 v, uint32_t c)
 #ifndef RNS_STREAM_RX_OCC  // waves/SIMD bound of the receive-verify instantiation (its finish needs registers)
 #define RNS_STREAM_RX_OCC 6
 #endif
+#ifndef RNS_STREAM_RX_NTSTORE  // A/B knob: nontemporal status stores in the stream receive verify
+#define RNS_STREAM_RX_NTSTORE 0
+#endif
 #ifndef RNS_STREAM_OUT  // A/B knob: result stores (0 plain, 1 nontemporal, 2 diagnostic: none)
 #define RNS_STREAM_OUT 1
 #endif
@@ -1995,7 +1998,7 @@ csum_stream_kernel(
 {
     static_assert(MODE == kStashNone || MODE == kStashHead, "stream modes: plain, receive verify");
     static_assert(KS == 1 || KS == 2 || KS == 4, "packet sets per wave");
-    static_assert(!XO || (MODE == kStashNone && KS == 1 && BUF && kStreamD >= 4), "XO: plain mode, one set, buffers");
+    static_assert(!XO || (KS == 1 && BUF && kStreamD >= 4), "XO: one set per wave, buffers");
     constexpr bool RX = MODE == kStashHead;
     constexpr int kNS = RX ? 5 : 1;  // stash chunks per datagram (the unaligned path fills 5)
     constexpr uint32_t kNP = 64u * KS;
@@ -2065,17 +2068,35 @@ csum_stream_kernel(
         if (persist)
             load_desc(u_next);
     };
-    // XO: the results as buffer stores (out-of-range offset: dropped by the hardware, no traffic)
+    // XO: the results as buffer stores (out-of-range offset: dropped by the hardware, no traffic);
+    // receive verify: the u8 statuses, and the u16 L4 sums when asked for
     const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        a.out, static_cast<short>(0), static_cast<int>(XO ? 2u * a.n : 0u), 0x00020000);
+        RX ? static_cast<void *>(a.status) : static_cast<void *>(a.out), static_cast<short>(0),
+        static_cast<int>(XO ? (RX ? 1u : 2u) * a.n : 0u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t l4_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        a.l4_out, static_cast<short>(0), static_cast<int>((XO && RX && a.l4_out) ? 2u * a.n : 0u), 0x00020000);
+    uint32_t pend_l4 = 0;
+    uint64_t pend_l4_base = ~0ull;
     auto xo_store = [&](bool real) {
         const uint64_t p = pend_base + lane;
         const bool ok = real && pend_base != ~0ull && p < a.n;
-        __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(pend_res[0]), out_rsrc,
-                                              ok ? static_cast<uint32_t>(2 * p) : kOobOffset, 0,
-                                              RNS_STREAM_OUT == 1 ? kNtAux : 0);
+        if constexpr (RX)
+            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(pend_res[0]), out_rsrc,
+                                                 ok ? static_cast<uint32_t>(p) : kOobOffset, 0,
+                                                 RNS_STREAM_RX_NTSTORE ? kNtAux : 0);
+        else
+            __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(pend_res[0]), out_rsrc,
+                                                  ok ? static_cast<uint32_t>(2 * p) : kOobOffset, 0,
+                                                  RNS_STREAM_OUT == 1 ? kNtAux : 0);
         if (real)
             pend_base = ~0ull;
+    };
+    auto xo_store_l4 = [&]() {  // receive verify: the L4 sums (a null l4_out: 0 records, dropped)
+        const uint64_t p = pend_l4_base + lane;
+        const bool ok = pend_l4_base != ~0ull && p < a.n;
+        __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(pend_l4), l4_rsrc,
+                                              ok ? static_cast<uint32_t>(2 * p) : kOobOffset, 0, 0);
+        pend_l4_base = ~0ull;
     };
     // XO: extra operation j of the first row block (j < 4), a dropped store otherwise
     auto xo_op = [&](int j, bool first_block, uint64_t u_next) {
@@ -2090,6 +2111,8 @@ csum_stream_kernel(
             nx_r0 = a.blk_off[((ub * kNP) >> 6) + zero_v];
         } else if (j == 2) {
             nx_len[0] = static_cast<uint32_t>(a.len16[q]);  // (zeroed past the end at the unit's start)
+        } else if constexpr (RX) {
+            xo_store_l4();
         } else {
             if (a.seed)
                 nx_seed[0] = static_cast<uint32_t>(a.seed[q]);
@@ -2289,10 +2312,10 @@ csum_stream_kernel(
                 const uint8_t stv = rx_finish<kNS>(a, stash + (64u * i + lane) * kNS, mine[i],
                                                    static_cast<uint32_t>(start & 15), len[i], odd, false,
                                                    live && ok && len[i] != 0, l4_res);
-#ifndef RNS_STREAM_RX_NTSTORE  // A/B knob: nontemporal status stores in the stream receive verify
-#define RNS_STREAM_RX_NTSTORE 0
-#endif
-                if (live) {
+                if constexpr (XO) {  // stored after the next unit's first rows
+                    pend_res[0] = stv;
+                    pend_l4 = l4_res;
+                } else if (live) {
                     if constexpr (RNS_STREAM_RX_NTSTORE != 0)
                         __builtin_nontemporal_store(stv, a.status + p);
                     else
@@ -2309,12 +2332,16 @@ csum_stream_kernel(
                 }
             }
         }
-        if constexpr (!RX)
+        if constexpr (!RX || XO)
             pend_base = base;
+        if constexpr (RX && XO)
+            pend_l4_base = base;
         wave_lds_fence();  // the next range rewrites tab / pend / stash
     }
     if constexpr (XO) {
         xo_store(true);
+        if constexpr (RX)
+            xo_store_l4();
     } else if constexpr (!RX) {
         if (pend_base != ~0ull)
             store_results(pend_base, pend_res);
@@ -2536,10 +2563,10 @@ int launch_stream(const CsumArgs &a, int ks, hipStream_t st)
     if constexpr (MODE == kStashNone && RNS_STREAM_KS > 1) {
         (void)ks;
         RNS_LAUNCH_STREAM(RNS_STREAM_KS);
-    } else if (MODE == kStashNone && RNS_STREAM_XO && buf && grid.x < all_units && a.n < (1u << 31)) {
+    } else if (RNS_STREAM_XO && buf && grid.x < all_units && a.n < (1u << 30)) {  // (result offsets below kOobOffset)
         // a capped grid on the buffer path: the extra-operation-per-row form (delayed stores,
         // next unit's descriptors in flight)
-        hipLaunchKernelGGL((csum_stream_kernel<kStashNone, 1, NT, true, true>), grid, block, 0, st, a);
+        hipLaunchKernelGGL((csum_stream_kernel<MODE, 1, NT, true, true>), grid, block, 0, st, a);
     } else {
         (void)ks;  // (receive verify: always one set per wave — its stash is 5 chunks per datagram)
         RNS_LAUNCH_STREAM(1);

@@ -18,7 +18,8 @@ for v in main rnt; do
   if [ $v = main ]; then E=""; else E="RNS_CHECKSUM_LIB=$A$v.so"; fi
   steps+=(c2_$v 200 "$E python bench.py $B --config c2_64B --steps 200")
 done
-for v in main rxnt; do
+steps+=(py_rxp8 300 "RNS_CHECKSUM_LIB=${A}rxp8.so python -u -m pytest tests/test_gpu_rx.py tests/test_gpu_packed.py tests/test_gpu_bench_verify.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread")
+for v in main rxnt rxp8; do
   if [ $v = main ]; then E=""; else E="RNS_CHECKSUM_LIB=$A$v.so"; fi
   steps+=(v_c2_$v 200 "$E python bench.py $B --config c2_64B --op verify --steps 200")
 done
