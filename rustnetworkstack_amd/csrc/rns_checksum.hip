@@ -2348,6 +2348,217 @@ csum_stream_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Fragment chains in rounds (util.rs:112-119 over NetBuffer fragments, buf.rs:466-487):
+// the form for NetBuffer-sized fragments (typical length >= 384 B).  A wave owns 64
+// consecutive packets; their fragments (the CSR range) are taken up to kChainFB at a time,
+// descriptors parked in LDS.  Each half-wave (32 lanes) sums one fragment per round, one
+// 16-byte chunk per lane — a fragment of up to 496 bytes at any start is one round, longer
+// ones take ceil(chunks/32) rounds — with D rounds in flight, fragments j = g, g+2, ... for
+// half g.  The half's 32 chunk sums reduce with DPP (row_shr 1-8, row_bcast:15) into lanes
+// 31 / 63; the fragment's LE word sum (exact: <= 128 KiB) is folded and byte-order corrected
+// by the fragment's start parity (RFC 1071 §2(B)) into the reference's per-fragment BE sum
+// mod 0xffff, parked in LDS, and each packet's owner lane folds its fragments in order as
+// util.rs:114-116 does.  A sub-batch holding a fragment past 128 KiB (the reference's u32
+// can wrap) sums its fragments one at a time with the exact big-endian path instead.
+// ---------------------------------------------------------------------------
+#ifndef RNS_CHAIN_FB
+#define RNS_CHAIN_FB 128
+#endif
+#ifndef RNS_CHAIN_RD  // rounds in flight
+#define RNS_CHAIN_RD 4
+#endif
+#ifndef RNS_CHAIN_ROUNDS_OCC
+#define RNS_CHAIN_ROUNDS_OCC 8
+#endif
+constexpr uint32_t kChainFB = RNS_CHAIN_FB;
+constexpr int kChainRD = RNS_CHAIN_RD;
+
+template <bool NT, bool BUF>
+__global__ __launch_bounds__(64, RNS_CHAIN_ROUNDS_OCC) void csum_chain_rounds_kernel(const CsumArgs a)
+{
+    __shared__ uint4 finfo[kChainFB];    // per fragment: aligned start (lo, hi), length, [3:0] start & 15
+    __shared__ uint32_t fsum[kChainFB];  // per fragment: the BE sum (folded unless big)
+    __shared__ uint32_t fflag[kChainFB]; // per fragment: 1 = big (exact u32 sum), 2 = outside the arena
+    const uint32_t lane = threadIdx.x;
+    const uint32_t half = lane >> 5, hl = lane & 31;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
+    const uint64_t recs = buf_records(a);
+    constexpr uint32_t kBad = 0x80000000u;
+
+    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * 64;
+    const uint64_t p = base + lane;
+    const bool live = p < a.n;
+    uint32_t f0 = live ? a.first[p] : 0u, f1 = live ? a.first[p + 1] : 0u;
+    const bool rng_ok = f0 <= f1 && f1 <= a.n_frags;
+    if (!rng_ok)
+        f0 = f1 = 0;
+    uint32_t acc = ((a.seed && live) ? static_cast<uint32_t>(a.seed[p]) : 0u) | (rng_ok ? 0u : kBad);  // util.rs:113
+    const uint32_t F0 = wave_min_u32(f0 < f1 ? f0 : 0xFFFFFFFFu);
+    const uint32_t F1 = wave_max_u32(f0 < f1 ? f1 : 0u);
+    for (uint64_t fb = F0; fb < F1; fb += kChainFB) {
+        const uint32_t nf = static_cast<uint32_t>(min(static_cast<uint64_t>(kChainFB), F1 - fb));
+        // ---- the sub-batch's descriptors into LDS ----
+        bool any_big = false;
+#pragma unroll
+        for (uint32_t q = 0; q < kChainFB / 64; ++q) {
+            const uint32_t j = 64 * q + lane;
+            if (j < nf) {
+                const uint64_t foff = a.off[fb + j] + a.base_adjust;
+                const uint32_t flen = a.len[fb + j];
+                const bool fok = foff <= a.arena_bytes && flen <= a.arena_bytes - foff;
+                const uint32_t L = fok ? flen : 0u;
+                const uint64_t st = fok ? foff : 0;
+                finfo[j] = make_uint4(static_cast<uint32_t>(st & ~15ull), static_cast<uint32_t>(st >> 32), L,
+                                      static_cast<uint32_t>(st & 15));
+                fsum[j] = 0;
+                fflag[j] = (fok ? 0u : 2u) | (L > kNoWrapBytes ? 1u : 0u);
+                any_big = any_big || L > kNoWrapBytes;
+            }
+        }
+        wave_lds_fence();
+        if (!__ballot(any_big)) {
+            // ---- rounds: half g sums fragments g, g+2, ... one 32-chunk pass per round ----
+            // cursors (identical within a half): the issue cursor runs D rounds ahead of consumption
+            uint32_t ij = half, ip = 0;  // issue: fragment, pass
+            uint32_t lacc = 0;           // the consumed fragment's LE sum so far
+            uint4 v[kChainRD];
+            uint32_t inf[kChainRD];      // [0] valid, [1] last pass, [2] odd start, [10:3] fragment, [14:11] lo, [19:15] hi
+            auto issue = [&](uint4 &dst, uint32_t &info) {
+                uint64_t off = recs;  // past the arena: no load
+                info = 0;
+                if (ij < nf) {
+                    const uint4 fi = finfo[ij];
+                    const uint32_t nch = fi.z ? (fi.w + fi.z + 15) >> 4 : 0u;
+                    const uint32_t passes = max(1u, (nch + 31) >> 5);
+                    const uint32_t c = ip * 32 + hl;
+                    const uint32_t lo = c == 0 ? fi.w : 0u;
+                    const uint32_t hi = c + 1 == nch ? ((fi.w + fi.z - 1) & 15u) + 1u : 16u;
+                    if (c < nch)
+                        off = ((static_cast<uint64_t>(fi.y) << 32) | fi.x) + (static_cast<uint64_t>(c) << 4);
+                    info = 1u | (ip + 1 == passes ? 2u : 0u) | ((fi.w & 1u) << 2) | (ij << 3) | (lo << 11) |
+                           ((c < nch ? hi : 16u) << 15);
+                    if (++ip == passes) {
+                        ip = 0;
+                        ij += 2;
+                    }
+                }
+                const bool in = off + 16 <= recs;
+                if constexpr (BUF) {
+                    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(
+                        rsrc, in ? static_cast<uint32_t>(off) : kOobOffset, 0, NT ? kNtAux : 0);
+                    dst = make_uint4(x.x, x.y, x.z, x.w);
+                } else {
+                    const uint4 x = load_chunk<NT>(a.arena + (in ? off : 0));
+                    dst = in ? x : make_uint4(0, 0, 0, 0);
+                }
+            };
+#pragma unroll
+            for (int r = 0; r < kChainRD; ++r) {
+                issue(v[r], inf[r]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            while (__ballot(inf[0] & 1u)) {
+#pragma unroll
+                for (int r = 0; r < kChainRD; ++r) {
+                    const uint32_t in = inf[r];
+                    uint4 x = v[r];
+                    const uint32_t lo = (in >> 11) & 15u, hi = (in >> 15) & 31u;
+                    if (__ballot(lo != 0 || hi != 16)) {  // a fragment starts or ends inside a chunk here
+                        x.x = keep_bytes(x.x, static_cast<int>(lo), static_cast<int>(hi), 0);
+                        x.y = keep_bytes(x.y, static_cast<int>(lo), static_cast<int>(hi), 4);
+                        x.z = keep_bytes(x.z, static_cast<int>(lo), static_cast<int>(hi), 8);
+                        x.w = keep_bytes(x.w, static_cast<int>(lo), static_cast<int>(hi), 12);
+                    }
+                    uint32_t s = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
+                    s = __builtin_amdgcn_sad_u16(x.y, 0, s);
+                    s = __builtin_amdgcn_sad_u16(x.z, 0, s);
+                    s = __builtin_amdgcn_sad_u16(x.w, 0, s);
+                    __builtin_amdgcn_sched_barrier(0);
+                    issue(v[r], inf[r]);  // the round D ahead into the registers this round freed
+                    __builtin_amdgcn_sched_barrier(0);
+                    // the half's 32 chunk sums: an inclusive scan within each half, totals in lanes 31 / 63
+                    uint32_t t = s;
+                    t += dpp_or_zero<0x111>(s);
+                    t += dpp_or_zero<0x112>(s);
+                    t += dpp_or_zero<0x113>(s);
+                    t += dpp_or_zero<0x114, 0xF, 0xE>(t);
+                    t += dpp_or_zero<0x118, 0xF, 0xC>(t);
+                    t += dpp_or_zero<0x142, 0xA, 0xF>(t);
+                    const uint32_t part = half ? __builtin_amdgcn_readlane(t, 63) : __builtin_amdgcn_readlane(t, 31);
+                    if (in & 1u) {
+                        lacc += part;
+                        if (in & 2u) {  // the fragment's last pass: fold, correct the byte order, park it
+                            const uint32_t xx = fold16(lacc);
+                            const uint32_t g = (in & 4u) ? xx : (((xx & 0xff) << 8) | (xx >> 8));
+                            if (hl == 0)
+                                fsum[(in >> 3) & 0xFFu] = g;
+                            lacc = 0;
+                        }
+                    }
+                }
+            }
+        } else {
+            // ---- a fragment past 128 KiB in this sub-batch: one fragment at a time, exact ----
+            for (uint32_t j = 0; j < nf; ++j) {
+                const uint4 fi = finfo[j];
+                const uint64_t st = ((static_cast<uint64_t>(fi.y) << 32) | fi.x) + fi.w;
+                const uint32_t L = fi.z;
+                if (L == 0)
+                    continue;
+                const Pkt k = make_pkt(st, L);
+                uint32_t hs = 0, ls = 0, le = 0;
+                for (uint32_t cc = 0; cc < k.nch; cc += 64) {
+                    uint4 wv[1];
+                    issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, wv);
+                    mask_edges<64, 1, 1>(k, cc + lane, wv);
+                    if (k.big)
+                        sum_be<1, 1>(wv, (st & 1) ? 0x01000100u : 0x00010001u, hs, ls);
+                    else
+                        le = sum_le<1, 1>(wv, le);
+                }
+                const uint32_t sum = group_allreduce<64>(k.big ? (hs << 8) + ls : le);
+                uint32_t gv = sum;
+                if (!k.big) {
+                    const uint32_t xx = fold16(sum);
+                    gv = (st & 1) ? xx : (((xx & 0xff) << 8) | (xx >> 8));
+                }
+                if (lane == 0)
+                    fsum[j] = gv;
+            }
+        }
+        wave_lds_fence();
+        // owner lanes: each packet's fragments inside [fb, fb + nf), in order (util.rs:114-116)
+        const uint64_t t0 = max(static_cast<uint64_t>(f0), fb);
+        const uint64_t t1 = min(static_cast<uint64_t>(f1), fb + nf);
+        for (uint64_t t = t0; t < t1; ++t) {
+            const uint32_t gv = fsum[t - fb], fv = fflag[t - fb];
+            const uint32_t bad = (acc & kBad) | ((fv & 2u) ? kBad : 0u);
+            uint32_t sm = (acc & 0xffffu) + gv;  // big: util.rs:89-99 mod 2^32; else <= 0x1fffe
+            if (fv & 1u) {
+                while (sm > 0xffff)  // util.rs:101-103
+                    sm = (sm & 0xffff) + (sm >> 16);
+            } else {
+                sm = (sm & 0xffff) + (sm >> 16);  // one end-around step folds it
+            }
+            acc = sm | bad;
+        }
+        wave_lds_fence();  // the next sub-batch rewrites finfo / fsum / fflag
+    }
+    uint32_t r = acc & 0xffffu;
+    if (a.flags & RNS_FLAG_COMPLEMENT)
+        r ^= 0xffff;
+    const bool ok = !(acc & kBad);
+    if (live)
+        a.out[p] = static_cast<uint16_t>(ok ? r : 0u);  // 64 consecutive u16: one 128-byte store
+    if (a.bad) {
+        const uint64_t rejected = __ballot(live && !ok);
+        if (rejected && lane == 0)
+            atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void splitmix64_fill_kernel(uint8_t *buf, uint64_t nbytes, uint64_t seed)
 {
     const uint64_t nwords = (nbytes + 7) / 8;
@@ -2586,7 +2797,11 @@ int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
 #ifndef RNS_STREAM_MAXLEN  // A/B knob: the stream kernel for typical lengths up to this
 #define RNS_STREAM_MAXLEN 1200
 #endif
-    if (RNS_STREAM && a.align_mask >= 15u && !tiny && (a.len_hint == 0 || a.len_hint <= RNS_STREAM_MAXLEN))
+#ifndef RNS_STREAM_TINY  // A/B knob: 1 = tiny packets take the stream kernel too
+#define RNS_STREAM_TINY 0
+#endif
+    if (RNS_STREAM && a.align_mask >= 15u && (!tiny || RNS_STREAM_TINY) &&
+        (a.len_hint == 0 || a.len_hint <= RNS_STREAM_MAXLEN))
         return launch_stream<kStashNone>(a, 1, st);
     const uint64_t batches = (static_cast<uint64_t>(a.n) + 63) / 64;  // one wave per 64 packets
     const uint64_t wpb = ((sh.variant & 4u) ? kMixedBlock<false> : kBlock) / 64;  // waves per workgroup
@@ -2865,6 +3080,21 @@ int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
     const bool buf = buf_records(a) < kOobOffset;
     // RNS_FLAG_CHAIN_RUNS: the run-checking kernel (buffer path; a hint, ignored otherwise)
     const bool runs = kChainRuns && (flags & RNS_FLAG_CHAIN_RUNS) && buf;
+#ifndef RNS_CHAIN_ROUNDS  // 0 = never the rounds kernel; 1 = for NetBuffer-sized fragments; 2 = also with the runs hint
+#define RNS_CHAIN_ROUNDS 1
+#endif
+    if (RNS_CHAIN_ROUNDS && (frag_len_hint ? frag_len_hint : 512u) >= 384u && (!runs || RNS_CHAIN_ROUNDS == 2)) {
+        const dim3 rgrid(static_cast<uint32_t>((static_cast<uint64_t>(n_pkts) + 63) / 64)), rblock(64);
+        if (nt && buf)
+            hipLaunchKernelGGL((csum_chain_rounds_kernel<true, true>), rgrid, rblock, 0, st, a);
+        else if (nt)
+            hipLaunchKernelGGL((csum_chain_rounds_kernel<true, false>), rgrid, rblock, 0, st, a);
+        else if (buf)
+            hipLaunchKernelGGL((csum_chain_rounds_kernel<false, true>), rgrid, rblock, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_chain_rounds_kernel<false, false>), rgrid, rblock, 0, st, a);
+        return hip_status(hipGetLastError());
+    }
 #define RNS_CHAIN_LAUNCH(KM)                                                                      \
     if (runs && nt)                                                                               \
         hipLaunchKernelGGL((csum_chain_kernel<true, true, KM, true>), grid, block, 0, st, a);     \
