@@ -1632,8 +1632,8 @@ __global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX
             res = d_ok ? static_cast<uint16_t>(mine) : static_cast<uint16_t>(0);  // finished (and stored) in-round
         else
             res = finalize_bits(mine, odd, big, d_seed, d_ok, a.flags);
-#ifndef RNS_MIXED_NTSTORE  // A/B knob: nontemporal result stores in the plain class kernel
-#define RNS_MIXED_NTSTORE 0
+#ifndef RNS_MIXED_NTSTORE  // nontemporal result stores in the plain class kernel (c3 232.4 -> 229.5 us per step, r03l)
+#define RNS_MIXED_NTSTORE 1
 #endif
         if (live && a.out) {
             if constexpr (RNS_MIXED_NTSTORE != 0 && !FILL && !RX && !TX)
@@ -2123,10 +2123,12 @@ csum_stream_kernel(
 
     for (uint64_t u = blockIdx.x; u < nunit; u += gridDim.x) {
         const uint64_t base = u * kNP;
-        const uint64_t r0 = ((static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nx_r0 >> 32)))
-                              << 32) |
-                             __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nx_r0))) +
-                            a.base_adjust;  // the wave's first packet
+        // (the lane intrinsics return int: widen through uint32_t, or an offset past 2 GiB sign-extends)
+        const uint64_t r0 =
+            ((static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nx_r0 >> 32))))
+              << 32) |
+             static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nx_r0)))) +
+            a.base_adjust;  // the wave's first packet
         uint32_t len[KS], seed[KS], excl[KS];
         uint32_t total = 0;  // the region's bytes (a multiple of 16 on the stream path)
 #pragma unroll
@@ -2279,8 +2281,9 @@ csum_stream_kernel(
                     const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
                     todo &= todo - 1;
                     const uint64_t st =
-                        (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start >> 32), o)) << 32) |
-                        __builtin_amdgcn_readlane(static_cast<uint32_t>(start), o);
+                        (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start >> 32), o)))
+                         << 32) |
+                        static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start), o));
                     const uint32_t L = __builtin_amdgcn_readlane(len[i], o);
                     const Pkt k = make_pkt(st, L);
                     uint32_t acc = 0;
@@ -3080,8 +3083,8 @@ int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
     const bool buf = buf_records(a) < kOobOffset;
     // RNS_FLAG_CHAIN_RUNS: the run-checking kernel (buffer path; a hint, ignored otherwise)
     const bool runs = kChainRuns && (flags & RNS_FLAG_CHAIN_RUNS) && buf;
-#ifndef RNS_CHAIN_ROUNDS  // 0 = never the rounds kernel; 1 = for NetBuffer-sized fragments; 2 = also with the runs hint
-#define RNS_CHAIN_ROUNDS 1
+#ifndef RNS_CHAIN_ROUNDS  // A/B knob: 0 = never the rounds kernel (measured slower on c3 layouts, r03l);
+#define RNS_CHAIN_ROUNDS 0   // 1 = for NetBuffer-sized fragments; 2 = also with the runs hint
 #endif
     if (RNS_CHAIN_ROUNDS && (frag_len_hint ? frag_len_hint : 512u) >= 384u && (!runs || RNS_CHAIN_ROUNDS == 2)) {
         const dim3 rgrid(static_cast<uint32_t>((static_cast<uint64_t>(n_pkts) + 63) / 64)), rblock(64);
