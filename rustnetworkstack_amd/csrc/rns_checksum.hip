@@ -1971,7 +1971,10 @@ __device__ __forceinline__ uint4 keep_first(uint4 v, uint32_t c)
 #ifndef RNS_STREAM_RX_NTSTORE  // A/B knob: nontemporal status stores in the stream receive verify
 #define RNS_STREAM_RX_NTSTORE 0
 #endif
-#ifndef RNS_STREAM_OUT  // A/B knob: result stores (0 plain, 1 nontemporal, 2 diagnostic: none)
+#ifndef RNS_STREAM_OUT_AUX  // cache-policy bits of the RNS_STREAM_OUT == 3 buffer stores
+#define RNS_STREAM_OUT_AUX 0
+#endif
+#ifndef RNS_STREAM_OUT  // A/B knob: result stores (0 plain, 1 nontemporal, 2 diagnostic: none, 3 buffer + aux)
 #define RNS_STREAM_OUT 1
 #endif
 constexpr int kStreamD = RNS_STREAM_D;
@@ -2042,6 +2045,11 @@ csum_stream_kernel(
 #pragma unroll
     for (int i = 0; i < KS; ++i)
         pend_res[i] = 0;
+    // XO (and the buffer-store A/B): the results as buffer stores (out-of-range offset: dropped
+    // by the hardware, no traffic)
+    const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        RX ? static_cast<void *>(a.status) : static_cast<void *>(a.out), static_cast<short>(0),
+        static_cast<int>((XO || RNS_STREAM_OUT == 3) ? (RX ? 1u : 2u) * a.n : 0u), 0x00020000);
     auto store_results = [&](uint64_t b, const uint32_t *res) {
 #pragma unroll
         for (int i = 0; i < KS; ++i) {
@@ -2052,6 +2060,9 @@ csum_stream_kernel(
 #elif RNS_STREAM_OUT == 2  // diagnostic ONLY (results not written): the cost of the result stores
                 if (res[i] == 0xFFFFFFFFu)
                     a.out[p] = 0;
+#elif RNS_STREAM_OUT == 3  // A/B: buffer stores with cache-policy bits RNS_STREAM_OUT_AUX
+                __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(res[i]), out_rsrc,
+                                                      static_cast<uint32_t>(2 * p), 0, RNS_STREAM_OUT_AUX);
 #else
                 a.out[p] = static_cast<uint16_t>(res[i]);  // 64 consecutive u16: one 128-byte store
 #endif
@@ -2068,11 +2079,7 @@ csum_stream_kernel(
         if (persist)
             load_desc(u_next);
     };
-    // XO: the results as buffer stores (out-of-range offset: dropped by the hardware, no traffic);
     // receive verify: the u8 statuses, and the u16 L4 sums when asked for
-    const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        RX ? static_cast<void *>(a.status) : static_cast<void *>(a.out), static_cast<short>(0),
-        static_cast<int>(XO ? (RX ? 1u : 2u) * a.n : 0u), 0x00020000);
     const __amdgpu_buffer_rsrc_t l4_rsrc = __builtin_amdgcn_make_buffer_rsrc(
         a.l4_out, static_cast<short>(0), static_cast<int>((XO && RX && a.l4_out) ? 2u * a.n : 0u), 0x00020000);
     uint32_t pend_l4 = 0;
