@@ -1971,11 +1971,14 @@ __device__ __forceinline__ uint4 keep_first(uint4 v, uint32_t c)
 #ifndef RNS_STREAM_RX_NTSTORE  // A/B knob: nontemporal status stores in the stream receive verify
 #define RNS_STREAM_RX_NTSTORE 0
 #endif
-#ifndef RNS_STREAM_OUT_AUX  // cache-policy bits of the RNS_STREAM_OUT == 3 buffer stores
-#define RNS_STREAM_OUT_AUX 0
+#ifndef RNS_STREAM_OUT_AUX  // cache-policy bits of the RNS_STREAM_OUT == 3 buffer stores (17 = sc0 | sc1)
+#define RNS_STREAM_OUT_AUX 17
 #endif
-#ifndef RNS_STREAM_OUT  // A/B knob: result stores (0 plain, 1 nontemporal, 2 diagnostic: none, 3 buffer + aux)
-#define RNS_STREAM_OUT 1
+// Result stores: 0 plain, 1 nontemporal, 2 DIAGNOSTIC (none), 3 buffer stores with the policy
+// bits above.  IMIX, isolated dispatch: plain 472 us, nontemporal 454-461, sc0|sc1 455.9
+// (r03i, r03o; sc0 alone 474, sc1 457, sc1|nt 461-466, sc0|nt 459-460).
+#ifndef RNS_STREAM_OUT
+#define RNS_STREAM_OUT 3
 #endif
 constexpr int kStreamD = RNS_STREAM_D;
 
@@ -2049,7 +2052,7 @@ csum_stream_kernel(
     // by the hardware, no traffic)
     const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
         RX ? static_cast<void *>(a.status) : static_cast<void *>(a.out), static_cast<short>(0),
-        static_cast<int>((XO || RNS_STREAM_OUT == 3) ? (RX ? 1u : 2u) * a.n : 0u), 0x00020000);
+        static_cast<int>((XO || RNS_STREAM_OUT == 3) && a.n < (1u << 30) ? (RX ? 1u : 2u) * a.n : 0u), 0x00020000);
     auto store_results = [&](uint64_t b, const uint32_t *res) {
 #pragma unroll
         for (int i = 0; i < KS; ++i) {
@@ -2060,9 +2063,12 @@ csum_stream_kernel(
 #elif RNS_STREAM_OUT == 2  // diagnostic ONLY (results not written): the cost of the result stores
                 if (res[i] == 0xFFFFFFFFu)
                     a.out[p] = 0;
-#elif RNS_STREAM_OUT == 3  // A/B: buffer stores with cache-policy bits RNS_STREAM_OUT_AUX
-                __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(res[i]), out_rsrc,
-                                                      static_cast<uint32_t>(2 * p), 0, RNS_STREAM_OUT_AUX);
+#elif RNS_STREAM_OUT == 3  // buffer stores with cache-policy bits RNS_STREAM_OUT_AUX (32-bit offsets)
+                if (a.n < (1u << 30))
+                    __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(res[i]), out_rsrc,
+                                                          static_cast<uint32_t>(2 * p), 0, RNS_STREAM_OUT_AUX);
+                else
+                    __builtin_nontemporal_store(static_cast<uint16_t>(res[i]), a.out + p);
 #else
                 a.out[p] = static_cast<uint16_t>(res[i]);  // 64 consecutive u16: one 128-byte store
 #endif
@@ -2719,8 +2725,11 @@ struct Shape {
 Shape pick_shape(uint32_t len_hint)
 {
     const uint32_t chunks = len_hint ? (len_hint + 15) / 16 + 1 : 96;
+#ifndef RNS_TINY_GRID  // A/B knob: workgroups (4 waves each) for tiny packets
+#define RNS_TINY_GRID 2048u
+#endif
     if (chunks <= 8)  // rounds, nontemporal, next batch's descriptors prefetched (c2: 15.1 -> 14.4 us)
-        return Shape{19u, 4u, 1u, 2048u};
+        return Shape{19u, 4u, 1u, RNS_TINY_GRID};
     if (chunks <= 48)
         return Shape{4u, 0u, 0u, RNS_MIXED_GRID_CAP};
     if (chunks <= 160)
@@ -3588,8 +3597,9 @@ const char *rns_csum_shape_name(uint32_t len_hint)
 
 const char *rns_build_info(void)
 {
-    return "rns_checksum abi=1 offload-arch=gfx950 kernels=csum_mixed_kernel (per-wave size-class sort; "
-           "verify / fill / transmit-finalize stash modes), csum_rounds_kernel, csum_batch_kernel, "
+    return "rns_checksum abi=1 offload-arch=gfx950 kernels=csum_stream_kernel (packed form: 1 KiB rows per "
+           "64-packet region, prefix sums per packet; plain and receive-verify modes), csum_mixed_kernel (per-wave "
+           "size-class sort; verify / fill / transmit-finalize stash modes), csum_rounds_kernel, csum_batch_kernel, "
            "csum_chain_kernel (one pass, per-fragment fold) (v_sad_u16 LE sums, v_dot4 BE sums past 128 KiB, wave64, "
            "DPP reductions)";
 }
