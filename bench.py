@@ -89,9 +89,10 @@ def parse_args(argv=None):
     p.add_argument("--graph-streams", type=int, default=0,
                    help="graph mode: steps alternate over this many streams (independent batches may overlap); "
                         "0 = auto: 3 for tiny packets (mean < 128 B: c2 11.15-11.19 us with 3, 11.2-11.5 with 2 or 4), "
-                        "4 for small mixed packets (mean < 1000 B: IMIX 405-424 us with 4, 422-430 with 3, 450-480 "
-                        "with 2), 2 otherwise (c3 and c4 equal for 2-6; profiles/r02_graph_overlap.json, "
-                        "r02_graph_streams.json)")
+                        "4 for small mixed packets (mean < 1000 B), 2 otherwise (c3 and c4 equal for 2-6; "
+                        "profiles/r02_graph_overlap.json, r02_graph_streams.json).  Every stream reads its own batch "
+                        "(cache-honest); with that, IMIX gains nothing from 2-4 streams (r03a: 491-498 us per step "
+                        "either way; round 2's 405-424 us with 4 streams over ONE arena was partly cache-served)")
     p.add_argument("--shard", default="",
                    help="r/N: one GPU runs rank r's packet-index shard of the config's batch as an N-rank strong-scaling "
                         "run would cut it (make_layout(config, shard=(r, N))) — the per-rank workload of the N-GPU "

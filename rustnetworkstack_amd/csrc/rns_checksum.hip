@@ -2725,11 +2725,14 @@ struct Shape {
 Shape pick_shape(uint32_t len_hint)
 {
     const uint32_t chunks = len_hint ? (len_hint + 15) / 16 + 1 : 96;
+#ifndef RNS_TINY_VARIANT  // A/B knob: 19 = rounds, nt, next batch's descriptors prefetched; 11 = every round in flight
+#define RNS_TINY_VARIANT 19u
+#endif
 #ifndef RNS_TINY_GRID  // A/B knob: workgroups (4 waves each) for tiny packets
 #define RNS_TINY_GRID 2048u
 #endif
     if (chunks <= 8)  // rounds, nontemporal, next batch's descriptors prefetched (c2: 15.1 -> 14.4 us)
-        return Shape{19u, 4u, 1u, RNS_TINY_GRID};
+        return Shape{RNS_TINY_VARIANT, 4u, 1u, RNS_TINY_GRID};
     if (chunks <= 48)
         return Shape{4u, 0u, 0u, RNS_MIXED_GRID_CAP};
     if (chunks <= 160)
