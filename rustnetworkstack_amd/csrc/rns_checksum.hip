@@ -2784,6 +2784,11 @@ int launch_stream(const CsumArgs &a, int ks, hipStream_t st)
         units = std::min<uint64_t>(units, RNS_STREAM_TINY_CAP);
     if (RNS_STREAM_PERSIST)
         units = std::min<uint64_t>(units, static_cast<uint64_t>(device_cus()) * 4u * RNS_STREAM_PERSIST);
+#ifndef RNS_STREAM_UPW  // A/B knob: units per wave (grid = units / UPW, the XO form when > 1); 1 = one-shot
+#define RNS_STREAM_UPW 1
+#endif
+    if (RNS_STREAM_UPW > 1)
+        units = (units + RNS_STREAM_UPW - 1) / RNS_STREAM_UPW;
     const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(units, 0x7FFFFFFFu))), block(64);
     constexpr bool NT = RNS_STREAM_NT != 0;
 #define RNS_LAUNCH_STREAM(K)                                                                       \
