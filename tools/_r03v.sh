@@ -13,5 +13,5 @@ for rep in 1 2; do
     steps+=(v_c2_${v}_$rep 200 "$E python bench.py --no-cpu-baseline --no-host-pipeline --warmup 5 --steps 200 --config c2_64B --op verify")
   done
 done
-bash tools/gpu_steps.sh r03v "${steps[@]}"
+bash tools/gpu_steps.sh r03v "${steps[@]}" && \
 bash tools/pmc_configs.sh r03u c5_imix
