@@ -8,6 +8,8 @@ per GPU, already resident in HBM).  value = payload bytes checksummed by all
 ranks / max-over-ranks wall time of the K timed steps / 2^30.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3_1500B]
+        (N > 1 without a launcher: bench.py starts N ranks under torch.distributed.run itself,
+         as a child process, and exits with its code)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -679,11 +681,6 @@ def shard_leg(engine, args) -> dict:
                                           "(no peer GPU on a 1-GPU box), mean of 20"}}
 
 
-def _gpu_available() -> bool:
-    import torch
-    return torch.cuda.is_available()
-
-
 class _NoDist:
     """Single-process stand-in for Dist (the isolated re-measurement needs no barrier)."""
     enabled = False
@@ -704,8 +701,46 @@ def load_traffic(path: str, config: str):
     return t
 
 
+def launch_ranks(args, argv) -> int:
+    """`--gpus N` (N > 1) without a torch.distributed launcher: start N ranks of this
+    same script under `torch.distributed.run` as a CHILD process (never an exec: no
+    GPU has been touched yet, but the child must own the ranks, not this process),
+    relay its output and return its exit code.  The child sees WORLD_SIZE == N, so
+    its main() runs the ranks' path."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    script = os.path.abspath(sys.argv[0]) if sys.argv and sys.argv[0].endswith(".py") else os.path.abspath(__file__)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", script] + list(argv)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    print(f"bench.py: --gpus {args.gpus} without WORLD_SIZE: launching {args.gpus} ranks via torch.distributed.run",
+          file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def check_world(args) -> None:
+    """--gpus must agree with the launcher's WORLD_SIZE (a silent N=1 line for an N-GPU
+    request would be a wrong measurement)."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None and int(world) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher and --gpus disagree")
+
+
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     args = parse_args(argv)
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and os.environ.get("WORLD_SIZE") is None:
+        rc = launch_ranks(args, argv)  # before any torch.cuda / HIP call in this process
+        if rc != 0:
+            raise SystemExit(rc)
+        return None
+    check_world(args)
     dist = Dist()
     shape = tuple(int(x) for x in args.shape.split(",")) if args.shape else None
     strong = args.scaling == "strong" or (args.scaling == "auto" and args.config == "c5_imix")
@@ -716,13 +751,18 @@ def main(argv=None):
         raise SystemExit("--shard r/N is a one-process measurement of one rank's shard (use --scaling strong at N>1)")
     if args.shard_rw is not None:
         strong = True
-    use_graph = args.graph == "on" or (args.graph == "auto" and _gpu_available())
     if args.graph_streams <= 0:
         from rustnetworkstack_amd.workloads import make_layout
         args.graph_streams = auto_graph_streams(make_layout(args.config, n=4096).mean_len)
+    # min_batches is a hint for the graph path (one batch per graph stream); an engine
+    # that is not on a GPU ignores it, and the graph decision follows the engine's device
     engine = GpuEngine(args.config, dist.rank, dist.local_rank, shape=shape, steps=args.steps, world=dist.world,
                        strong=strong, compact=args.desc, op=args.op,
-                       min_batches=args.graph_streams if use_graph else 1, shard=args.shard_rw)
+                       min_batches=args.graph_streams if args.graph != "off" else 1, shard=args.shard_rw)
+    on_gpu = getattr(engine, "device", None) is not None and engine.device.type == "cuda"
+    if args.graph == "on" and not on_gpu:
+        raise SystemExit("bench.py: --graph on needs the GPU engine")
+    use_graph = args.graph == "on" or (args.graph == "auto" and on_gpu)
     graph = engine.capture(args.steps, args.graph_streams) if use_graph else None
     ramp_steps = clock_ramp(engine, args.ramp_s, graph=graph) if args.ramp_s > 0 else 0
     r = timed_loop(engine, dist, args.steps, args.warmup, graph=graph)

@@ -71,8 +71,10 @@ class CpuEngine(bench.GpuEngine):
         return "cpu stand-in"
 
 bench.GpuEngine = CpuEngine
-line = bench.main(["--config", {config!r}, "--steps", "3", "--warmup", "1", "--median-launches", "3",
+line = bench.main(["--gpus", "2", "--config", {config!r}, "--steps", "3", "--warmup", "1", "--median-launches", "3",
                    "--traffic-json", "/nonexistent/{{config}}.json"])
+if line is None:   # the launching parent (bench.py --gpus 2 without torchrun): the ranks did the work
+    sys.exit(0)
 eng = ENGINES[0]
 rank = int(os.environ["RANK"])
 with open(os.path.join({outdir!r}, f"rank{{rank}}.json"), "w") as f:   # (stdout lines of 2 ranks interleave)
@@ -89,13 +91,21 @@ def free_port():
     return p
 
 
-@pytest.mark.parametrize("config,n", [("c5_imix", 40001), ("c3_1500B", 3000)])
-def test_two_rank_gloo_bench_main(tmp_path, oracle, config, n):
+@pytest.mark.parametrize("config,n,launch", [("c5_imix", 40001, "torchrun"), ("c3_1500B", 3000, "torchrun"),
+                                             ("c5_imix", 20001, "self"), ("c3_1500B", 2000, "self")])
+def test_two_rank_gloo_bench_main(tmp_path, oracle, config, n, launch):
+    """launch = torchrun: the driver's N>1 command; self: a plain `python <script> --gpus 2`
+    (no WORLD_SIZE), where bench.py must start the two ranks itself."""
     script = tmp_path / "worker.py"
     script.write_text(WORKER.format(root=ROOT, n=n, config=config, outdir=str(tmp_path)))
     env = dict(os.environ, OMP_NUM_THREADS="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(script)]
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    if launch == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+               "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(script)]
+    else:
+        cmd = [sys.executable, str(script)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     res = {}
@@ -212,7 +222,7 @@ class CpuVerifyEngine(bench.GpuEngine):
         return "cpu stand-in"
 
 bench.GpuEngine = CpuVerifyEngine
-line = bench.main(["--config", {config!r}, "--op", "verify", "--steps", "2", "--warmup", "1",
+line = bench.main(["--gpus", "2", "--config", {config!r}, "--op", "verify", "--steps", "2", "--warmup", "1",
                    "--traffic-json", "/nonexistent/{{config}}.json"])
 rank = int(os.environ["RANK"])
 with open(os.path.join({outdir!r}, f"rank{{rank}}.json"), "w") as f:
@@ -249,3 +259,22 @@ def test_two_rank_gloo_verify_allreduce(tmp_path, config, n):
         assert k in line and line[k] > 0, k
     assert "value_gather" not in line
     assert line["cpu_baseline"] is None
+
+
+def test_gpus_disagreeing_with_world_size_fails(tmp_path):
+    """--gpus 2 under a launcher that says WORLD_SIZE=1 must exit non-zero, before any
+    engine is built (no silent one-rank line for a two-GPU request)."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert r.returncode != 0
+    assert "WORLD_SIZE=1" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_gpus_zero_rejected(tmp_path):
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "0", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert r.returncode != 0
