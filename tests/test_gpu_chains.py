@@ -69,6 +69,43 @@ def test_random_scattered_chains(oracle):
     assert np.array_equal(got, expect)
 
 
+def _c_caller_chains(n, seed):
+    """The distribution of tests/c/test_batch_abi.c test_chains, whose run in session r03h
+    caught add3326's chain stream kernel (tools/forensics/chain_stream_r03h.py):
+    0-6 fragments of 1-700 B per packet; half the packets scattered (gaps of 0-28 B, any
+    alignment), half back-to-back views with even non-final lengths (a run)."""
+    w = O.splitmix64_words(seed, n)
+    nfr = (w % np.uint64(7)).astype(np.int64)
+    adjacent = ((w >> np.uint64(8)) & np.uint64(1)).astype(bool)
+    first = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(nfr, out=first[1:])
+    nf = int(first[-1])
+    q = O.splitmix64_words(seed + 1, nf)
+    pk = np.repeat(np.arange(n), nfr)
+    j = np.arange(nf) - first[pk]
+    lens = (np.uint64(1) + (q >> np.uint64(8)) % np.uint64(700)).astype(np.int64)
+    run = adjacent[pk] & (j + 1 < nfr[pk])
+    lens = np.where(run, np.maximum(lens & ~1, 2), lens)
+    gaps = np.where(adjacent[pk], 0, (q % np.uint64(29)).astype(np.int64))
+    offs = np.cumsum(gaps + lens) - lens
+    seeds = ((w >> np.uint64(16)) & np.uint64(0xFFFF)).astype(np.uint16)
+    return offs.astype(np.uint64), lens.astype(np.uint32), first, seeds, int(offs[-1] + lens[-1]) + 32
+
+
+@pytest.mark.parametrize("hint", [0, 40, 350, 512, 1500])
+def test_c_caller_chain_distribution(oracle, hint):
+    """Every fragment-length hint (each kernel choice) on the C caller's chain mix, including
+    the last rows of every 64-fragment group (where the removed kernel lost chunks)."""
+    offs, lens, first, seeds, size = _c_caller_chains(20_000, 0xC11A + hint)
+    arena_np = O.splitmix64_bytes(0xC11B, size)
+    a = torch.from_numpy(arena_np).to(DEV)
+    for runs in (False, True):
+        expect = oracle.chain_batch(arena_np, offs, lens, first, seeds, complement=True)
+        got = host_u16(csum_chain(a, dev(offs, np.int64), dev(lens, np.int32), dev(first.astype(np.uint32), np.int32),
+                                  dev(seeds, np.int16), complement=True, frag_len_hint=hint, runs=runs))
+        assert np.array_equal(got, expect), (hint, runs, int(np.flatnonzero(got != expect)[0]))
+
+
 def test_full_size_received_fragments_match_contiguous(oracle):
     """Headline batch (1M x 1500 B) as the stack receives it after the IP trim
     ([492, 512, 476]-byte fragments): chain result == contiguous result == oracle."""
