@@ -30,7 +30,7 @@ per-launch mean (`kernel_avg_us`) from which `roofline.frac` is computed.  A
 rocprofv3 --kernel-trace of the same command reproduces it (tools/profile_bench.py
 reports the trace's per-dispatch mean and median of the same K launches).  Event
 pairs around single launches are NOT used for the figure: each pair measured
-≈5 µs above the dispatch rocprof records (profiles/r02_evpair_vs_rocprof_c3_1500B.json);
+≈5 µs above the dispatch rocprof records (profiles/archive/r02/r02_evpair_vs_rocprof_c3_1500B.json);
 `--median-launches N` still reports their median as a diagnostic.
 """
 from __future__ import annotations
@@ -81,18 +81,18 @@ def parse_args(argv=None):
     p.add_argument("--ramp-s", type=float, default=0.5,
                    help="before the W warmup steps, repeat the step (untimed) for this many seconds so the "
                         "GPU leaves its idle clock state: a 2.9 GB IMIX launch takes 505-550 us in the first "
-                        "~0.1 s of load and 493-496 us after it (profiles/r02_clock_ramp.json); 0 = off")
+                        "~0.1 s of load and 493-496 us after it (profiles/archive/r02/r02_clock_ramp.json); 0 = off")
     p.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                    help="launch the K timed steps (and the warmup) as one HIP graph of K kernel launches "
                         "(torch.cuda.CUDAGraph) alternating over --graph-streams streams: no host launch cost "
                         "between steps, and consecutive (independent) batches overlap one kernel's drain with the "
                         "next one's ramp (c2 13.5 -> 11.8 us per step, c3 -4 %%, c5 -1.5 %%, c4 -1.2 %%: "
-                        "profiles/r02_graph_overlap.json); auto = on (every rank, so N=1 and N>1 are timed alike)")
+                        "profiles/archive/r02/r02_graph_overlap.json); auto = on (every rank, so N=1 and N>1 are timed alike)")
     p.add_argument("--graph-streams", type=int, default=0,
                    help="graph mode: steps alternate over this many streams (independent batches may overlap); "
                         "0 = auto: 3 for tiny packets (mean < 128 B: c2 11.15-11.19 us with 3, 11.2-11.5 with 2 or 4), "
                         "4 for small mixed packets (mean < 1000 B), 2 otherwise (c3 and c4 equal for 2-6; "
-                        "profiles/r02_graph_overlap.json, r02_graph_streams.json).  Every stream reads its own batch "
+                        "profiles/archive/r02/r02_graph_overlap.json, r02_graph_streams.json).  Every stream reads its own batch "
                         "(cache-honest); with that, IMIX gains nothing from 2-4 streams (r03a: 491-498 us per step "
                         "either way; round 2's 405-424 us with 4 streams over ONE arena was partly cache-served)")
     p.add_argument("--shard", default="",
@@ -123,7 +123,7 @@ def parse_args(argv=None):
 
 
 def auto_graph_streams(mean_len: float) -> int:
-    """Streams the graph-mode timed steps alternate over (profiles/r02_graph_streams.json, and
+    """Streams the graph-mode timed steps alternate over (profiles/archive/r02/r02_graph_streams.json, and
     r03 with every concurrently running step reading its own batch): 3 for tiny packets, 4 for
     small mixed ones, 2 for MTU and jumbo batches."""
     return 3 if mean_len < 128 else 4 if mean_len < 1000 else 2
@@ -146,11 +146,13 @@ class Dist:
             self.local_rank = int(os.environ["RNS_BENCH_DEVICE"])
         backend = backend or os.environ.get("RNS_BENCH_BACKEND") or None
         self.enabled = self.world > 1
-        if self.enabled and torch.cuda.is_available():
-            torch.cuda.set_device(self.local_rank)  # before RCCL binds its communicator
+        if self.enabled:
+            backend = backend or ("nccl" if torch.cuda.is_available() else "gloo")
+            if backend == "nccl":
+                torch.cuda.set_device(self.local_rank)  # before RCCL binds its communicator
         if self.enabled and not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group(backend=backend or ("nccl" if torch.cuda.is_available() else "gloo"))
+            dist.init_process_group(backend=backend)
         self.backend = dist.get_backend() if self.enabled else None
         self.torch = torch
 
@@ -506,12 +508,15 @@ class GpuEngine:
         from rustnetworkstack_amd import _lib
         if self.op == "verify":
             if self.verify_packed:
+                if self.layout.n and self.layout.arena_bytes // self.layout.n <= 128:  # the library's ACK-sized rule
+                    return ("rx_rows_kernel (rns_rx_verify_packed_dev, ACK-sized datagrams: owners load their "
+                            "datagrams whole)")
                 return "csum_stream_kernel<RX> (rns_rx_verify_packed_dev: 1 KiB rows + header stash)"
             return "csum_mixed_kernel<RX> (rns_rx_verify_dev: class-sorted data pass + header stash)"
         mean = self.layout.mean_len
         if self.packed and self.layout.n and int(self.layout.off[0]) % 16 == 0 and 112 < mean <= 1200:
-            return ("csum_stream_kernel (packed form, 16-byte-aligned packets: one wave streams each 64-packet "
-                    "block as 1 KiB rows, prefix sums per packet)")
+            return ("csum_rows_kernel (packed form, 16-byte-aligned packets: one wave streams each 64-packet "
+                    "block as 1 KiB rows; owners capture two region prefixes and sum their own end chunk)")
         return _lib.load().rns_csum_shape_name(int(round(self.layout.mean_len))).decode()
 
     def out_sample(self, count: int):

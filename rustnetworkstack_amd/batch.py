@@ -38,6 +38,25 @@ def _require_cuda(t: torch.Tensor, name: str, dtypes) -> None:
 _U16 = (torch.uint16, torch.int16)
 
 
+def _rx_outputs(dev: torch.device, n: int, status, l4_sum, inputs):
+    """Receive verify's outputs (caller-supplied or new) and its inputs' device: the kernel
+    writes n entries to each output, so an undersized or misplaced buffer is refused."""
+    for name, t in inputs:
+        if t.device != dev:
+            raise ValueError(f"{name} is on {t.device}, the arena on {dev}")
+    if status is None:
+        status = torch.empty(n, dtype=torch.uint8, device=dev)
+    else:
+        _require_cuda(status, "status", (torch.uint8,))
+        if status.numel() != n or status.device != dev:
+            raise ValueError(f"status must be {n} uint8 entries on {dev}")
+    if l4_sum is not None:
+        _require_cuda(l4_sum, "l4_sum", _U16)
+        if l4_sum.numel() != n or l4_sum.device != dev:
+            raise ValueError(f"l4_sum must be {n} 16-bit entries on {dev}")
+    return status, (l4_sum.data_ptr() if l4_sum is not None else None)
+
+
 def _stream_handle(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
@@ -377,14 +396,11 @@ def rx_verify(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, loca
     if len(local_ipv4) != 4 or len(local_ipv6) != 16:
         raise ValueError("local_ipv4 must be 4 bytes and local_ipv6 16 bytes")
     n = off.numel()
+    if length.numel() != n:
+        raise ValueError("off and length must have the same number of datagrams")
     dev = arena.device
     lib = _lib.load()
-    if status is None:
-        status = torch.empty(n, dtype=torch.uint8, device=dev)
-    l4_ptr = None
-    if l4_sum is not None:
-        _require_cuda(l4_sum, "l4_sum", _U16)
-        l4_ptr = l4_sum.data_ptr()
+    status, l4_ptr = _rx_outputs(dev, n, status, l4_sum, (("off", off), ("length", length)))
     with torch.cuda.device(dev):
         st = lib.rns_rx_verify_dev(arena.data_ptr(), arena.numel(), off.data_ptr(), length.data_ptr(), n,
                                    bytes(local_ipv4), bytes(local_ipv6), status.data_ptr(), l4_ptr,
@@ -409,12 +425,7 @@ def rx_verify_packed(arena: torch.Tensor, blk_off: torch.Tensor, len16: torch.Te
         raise ValueError("blk_off needs one offset per 64 datagrams")
     dev = arena.device
     lib = _lib.load()
-    if status is None:
-        status = torch.empty(n, dtype=torch.uint8, device=dev)
-    l4_ptr = None
-    if l4_sum is not None:
-        _require_cuda(l4_sum, "l4_sum", _U16)
-        l4_ptr = l4_sum.data_ptr()
+    status, l4_ptr = _rx_outputs(dev, n, status, l4_sum, (("blk_off", blk_off), ("len16", len16)))
     with torch.cuda.device(dev):
         st = lib.rns_rx_verify_packed_dev(arena.data_ptr(), arena.numel(), blk_off.data_ptr(), len16.data_ptr(),
                                           int(align_log2), n, bytes(local_ipv4), bytes(local_ipv6),

@@ -38,6 +38,12 @@
 
 #include "rns_checksum.h"
 
+// Diagnostic A/B builds leave work out on purpose (wrong results) to measure what it costs.
+// They must never be mistaken for the product: each needs RNS_DIAGNOSTIC_BUILD as well.
+#if (defined(RNS_DIAG_NOSEED) || defined(RNS_FILL_NOSTORE)) && !defined(RNS_DIAGNOSTIC_BUILD)
+#error "RNS_DIAG_NOSEED and RNS_FILL_NOSTORE give wrong results: add -DRNS_DIAGNOSTIC_BUILD"
+#endif
+
 namespace {
 
 #ifndef RNS_BLOCK
@@ -72,7 +78,7 @@ struct CsumArgs {
     const uint32_t *first;     // fragment chains: packet i = fragments [first[i], first[i+1]) (off/len = fragments)
     uint32_t n_frags;
     uint32_t chain_k;          // fragment chains: packets per lane (a wave owns 64*chain_k consecutive packets)
-    uint32_t len_hint;         // packed form: the caller's typical packet length (stream kernel packet sets)
+    uint32_t len_hint;         // packed form: the caller's typical packet length (kernel choice)
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -1423,7 +1429,13 @@ template <bool STRIDED, bool NT, bool BUF, bool FILL, bool RX = false, bool TX =
 #ifndef RNS_STASH_OCC  // waves/SIMD bound of the stash modes (receive verify, transmit fill/finalize)
 #define RNS_STASH_OCC 4
 #endif
-__global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX && !TX) ? RNS_MIXED_OCC : RNS_STASH_OCC) void csum_mixed_kernel(const CsumArgs a)
+#ifndef RNS_FILL_OCC  // waves/SIMD bound of transmit fill / finalize: 3 (4 spilled 8-84 B/lane; equal
+#define RNS_FILL_OCC 3      // time: c3 fill 346 / 348 us, IMIX 788 / 785, session r04b)
+#endif
+__global__ __launch_bounds__(kMixedBlock<FILL || RX || TX>, (BUF && !FILL && !RX && !TX) ? RNS_MIXED_OCC
+                                                             : (FILL || TX)                 ? RNS_FILL_OCC
+                                                                                            : RNS_STASH_OCC) void
+csum_mixed_kernel(const CsumArgs a)
 {
     static_assert(int(FILL) + int(RX) + int(TX) <= 1 && !(STRIDED && (RX || TX)), "one mode at a time");
     constexpr int kMode = RX ? kStashHead : FILL ? kStashField : TX ? kStashTx : kStashNone;
@@ -1962,616 +1974,547 @@ __device__ __forceinline__ uint4 keep_first(uint4 v, uint32_t c)
 #ifndef RNS_STREAM_D  // rows (1 KiB loads) in flight per wave
 #define RNS_STREAM_D 4
 #endif
-#ifndef RNS_STREAM_OCC  // waves/SIMD bound
-#define RNS_STREAM_OCC 8
-#endif
 #ifndef RNS_STREAM_RX_OCC  // waves/SIMD bound of the receive-verify instantiation (its finish needs registers)
 #define RNS_STREAM_RX_OCC 6
 #endif
-#ifndef RNS_STREAM_RX_NTSTORE  // A/B knob: nontemporal status stores in the stream receive verify
-#define RNS_STREAM_RX_NTSTORE 0
-#endif
-#ifndef RNS_STREAM_OUT_AUX  // cache-policy bits of the RNS_STREAM_OUT == 3 buffer stores (17 = sc0 | sc1)
+#ifndef RNS_STREAM_OUT_AUX  // cache-policy bits of the result buffer stores (17 = sc0 | sc1)
 #define RNS_STREAM_OUT_AUX 17
 #endif
-// Result stores: 0 plain, 1 nontemporal, 2 DIAGNOSTIC (none), 3 buffer stores with the policy
-// bits above.  IMIX, isolated dispatch: plain 472 us, nontemporal 454-461, sc0|sc1 455.9
-// (r03i, r03o; sc0 alone 474, sc1 457, sc1|nt 461-466, sc0|nt 459-460).
-#ifndef RNS_STREAM_OUT
-#define RNS_STREAM_OUT 3
-#endif
+// Result stores: buffer stores with the policy bits above (arrays below 2^30 entries; larger
+// ones: nontemporal stores).  IMIX, isolated dispatch: plain stores 472 us, nontemporal
+// 454-461, sc0|sc1 455.9 (r03i, r03o; sc0 alone 474, sc1 457, sc1|nt 461-466, sc0|nt 459-460).
 constexpr int kStreamD = RNS_STREAM_D;
 
-// MODE kStashNone: the plain batch checksum (seed, optional complement, u16 out).
-// MODE kStashHead: receive verify (rns_rx_verify_packed_dev): the lanes that load a
-// datagram's first 4 chunks (64 bytes: every IPv4 header incl. options, the IPv6 header)
-// also copy them to an LDS stash, and the owner finishes exactly as the class kernel's
-// receive verify does (rx_finish).
-// KS: 64-packet sets per wave.  The wave's region is its KS*64 packets' bytes, streamed
-// as one row sequence: small packets (IMIX, ACKs) give a wave KS times the bytes, so the
-// per-wave start (descriptor load, first row latency) and end are paid KS times less
-// often.  Lane l owns packets 64*i + l of the wave's range (i < KS).
-// XO (capped grid, plain mode, buffer path): every row step issues exactly one extra memory
-// operation after its row load — the previous unit's result store, one of the next unit's
-// three descriptor loads, or an out-of-range (dropped) buffer store — so the vmcnt pattern
-// is the same for every row of every unit and the compiler's counted waits stay exact
-// (vmcnt(2D-1)); extra operations issued only at a unit's start would merge into the loop's
-// steady state as a wait for all D rows in flight.
-template <int MODE, int KS, bool NT, bool BUF, bool XO = false>
-__global__ __launch_bounds__(64, MODE == kStashHead ? RNS_STREAM_RX_OCC : KS == 4 ? 5 : RNS_STREAM_OCC) void
-csum_stream_kernel(
-    const CsumArgs a)
+// Receive verify (rns_rx_verify_packed_dev) of datagrams larger than ACKs: the lanes that
+// load a datagram's first 4 chunks (64 bytes: every IPv4 header incl. options, the IPv6
+// header) also copy them to an LDS stash, and the owner finishes exactly as the class
+// kernel's receive verify does (rx_finish).  (Round 3's plain mode of this kernel gave way
+// to csum_rows_kernel in round 4; forms that gave a wave several units were measured slower
+// in round 3 and removed.)  One wave per 64-datagram unit.
+template <bool NT, bool BUF>
+__global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(const CsumArgs a)
 {
-    static_assert(MODE == kStashNone || MODE == kStashHead, "stream modes: plain, receive verify");
-    static_assert(KS == 1 || KS == 2 || KS == 4, "packet sets per wave");
-    static_assert(!XO || (KS == 1 && BUF && kStreamD >= 4), "XO: one set per wave, buffers");
-    constexpr bool RX = MODE == kStashHead;
-    constexpr int kNS = RX ? 5 : 1;  // stash chunks per datagram (the unaligned path fills 5)
-    constexpr uint32_t kNP = 64u * KS;
+    constexpr int kNS = 5;  // stash chunks per datagram (the unaligned path fills 5)
     // entry bits: [31:17] row tag, [16] head chunk, [15:14] head index, [13] end chunk,
-    // [12] first chunk, [11:4] packet (of the wave's KS*64), [3:0] valid bytes - 1 (end chunk)
+    // [12] first chunk, [11:4] packet (of the wave's 64), [3:0] valid bytes - 1 (end chunk)
     constexpr uint32_t kTagShift = 17, kHead = 1u << 16, kEnd = 1u << 13, kStart = 1u << 12;
-    __shared__ uint32_t tab[64];        // per row: the entry of the chunk lane l loads
-    __shared__ uint32_t pend[kNP];      // per packet: the region prefix through its last chunk
-    __shared__ uint32_t pstart[kNP];    // per packet: the region prefix before its first chunk
-    __shared__ uint4 stash[RX ? kNP * kNS : 1];
+    __shared__ uint32_t tab[64];     // per row: the entry of the chunk lane l loads
+    __shared__ uint32_t pend[64];    // per packet: the region prefix through its last chunk
+    __shared__ uint32_t pstart[64];  // per packet: the region prefix before its first chunk
+    __shared__ uint4 stash[64 * kNS];
     const uint32_t lane = threadIdx.x;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
     const uint64_t recs = buf_records(a);
-    const uint64_t nunit = (static_cast<uint64_t>(a.n) + kNP - 1) / kNP;
-    // A wave that owns several units (capped grid: host knob RNS_STREAM_PERSIST) loads the next
-    // unit's descriptors while it streams this one, and stores a unit's results only after the
-    // NEXT unit's first rows are issued: gfx9 counts stores in vmcnt, in order, so a store issued
-    // before a load makes every wait for that load wait for the store's write acknowledgement
-    // too, and a one-shot wave holds its slot until its store completes.
-    const bool persist = gridDim.x < nunit;
-    uint32_t nx_len[KS], nx_seed[KS];
-    uint64_t nx_r0 = 0;
+    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * 64;
+    const uint64_t p = base + lane;
+    const bool live = p < a.n;
+    const uint64_t q = live ? p : a.n - 1;  // branch-free descriptor loads
     // (the block offset is loaded per lane at an index the compiler cannot prove uniform: a
     // uniform load is moved to SGPRs right away, with a vmcnt(0) wait for every row in flight)
     const uint32_t zero_v = __builtin_amdgcn_mbcnt_lo(0u, 0u);
-    auto load_desc = [&](uint64_t uu) {  // branch-free: past the end re-reads the last unit
-        const uint64_t ub = uu < nunit ? uu : nunit - 1;
-        nx_r0 = a.blk_off[((ub * kNP) >> 6) + zero_v];
-#pragma unroll
-        for (int i = 0; i < KS; ++i) {
-            const uint64_t pp = ub * kNP + 64u * i + lane;
-            const uint64_t q = pp < a.n ? pp : a.n - 1;
-            nx_len[i] = pp < a.n ? static_cast<uint32_t>(a.len16[q]) : 0u;
-            nx_seed[i] = (!RX && a.seed && pp < a.n) ? static_cast<uint32_t>(a.seed[q]) : 0u;
-        }
-    };
-    load_desc(blockIdx.x);
-    uint32_t pend_res[KS];  // plain mode: the previous unit's results, not yet stored
-    uint64_t pend_base = ~0ull;
-#pragma unroll
-    for (int i = 0; i < KS; ++i)
-        pend_res[i] = 0;
-    // XO (and the buffer-store A/B): the results as buffer stores (out-of-range offset: dropped
-    // by the hardware, no traffic)
-    const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        RX ? static_cast<void *>(a.status) : static_cast<void *>(a.out), static_cast<short>(0),
-        static_cast<int>((XO || RNS_STREAM_OUT == 3) && a.n < (1u << 30) ? (RX ? 1u : 2u) * a.n : 0u), 0x00020000);
-    auto store_results = [&](uint64_t b, const uint32_t *res) {
-#pragma unroll
-        for (int i = 0; i < KS; ++i) {
-            const uint64_t p = b + 64u * i + lane;
-            if (p < a.n) {
-#if RNS_STREAM_OUT == 1  // nontemporal result stores (IMIX isolated 472 -> 454 us, r03i)
-                __builtin_nontemporal_store(static_cast<uint16_t>(res[i]), a.out + p);
-#elif RNS_STREAM_OUT == 2  // diagnostic ONLY (results not written): the cost of the result stores
-                if (res[i] == 0xFFFFFFFFu)
-                    a.out[p] = 0;
-#elif RNS_STREAM_OUT == 3  // buffer stores with cache-policy bits RNS_STREAM_OUT_AUX (32-bit offsets)
-                if (a.n < (1u << 30))
-                    __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(res[i]), out_rsrc,
-                                                          static_cast<uint32_t>(2 * p), 0, RNS_STREAM_OUT_AUX);
-                else
-                    __builtin_nontemporal_store(static_cast<uint16_t>(res[i]), a.out + p);
-#else
-                a.out[p] = static_cast<uint16_t>(res[i]);  // 64 consecutive u16: one 128-byte store
-#endif
+    const uint64_t r0v = a.blk_off[(base >> 6) + zero_v];
+    const uint32_t len = live ? static_cast<uint32_t>(a.len16[q]) : 0u;
+    // (the lane intrinsics return int: widen through uint32_t, or an offset past 2 GiB sign-extends)
+    const uint64_t r0 =
+        ((static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(r0v >> 32))))
+          << 32) |
+         static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(r0v)))) +
+        a.base_adjust;  // the wave's first packet
+    const uint32_t pad = (len + a.align_mask) & ~a.align_mask;
+    const uint32_t incl = wave_incl_scan(pad);
+    const uint32_t excl = incl - pad;
+    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);  // the region's bytes
+    uint32_t mine = 0;
+    bool odd = false;
+
+    if ((r0 & 15) == 0) {
+        // ---- stream path ----
+        const uint32_t nrows = (total + 1023) >> 10;
+        tab[lane] = 0xFFFFFFFFu;  // tag 0x7FFF: never a row
+        wave_lds_fence();
+        uint32_t carry = 0;
+        uint4 v[kStreamD];
+        auto issue = [&](uint32_t k, uint4 &dst) {  // row k: chunk 64k + lane of the region
+            const uint64_t off = r0 + (static_cast<uint64_t>(k) << 10) + (lane << 4);
+            const bool in = k < nrows && off + 16 <= recs;
+            if constexpr (BUF) {
+                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(
+                    rsrc, in ? static_cast<uint32_t>(off) : kOobOffset, 0, NT ? kNtAux : 0);
+                dst = make_uint4(x.x, x.y, x.z, x.w);
+            } else {
+                const uint4 x = load_chunk<NT>(a.arena + (in ? off : 0));
+                dst = in ? x : make_uint4(0, 0, 0, 0);
             }
-        }
-    };
-    // after this unit's first rows are issued: the previous unit's stores, the next unit's descriptors
-    auto overlap_point = [&](uint64_t u_next) {
-        if constexpr (!RX) {
-            if (pend_base != ~0ull)
-                store_results(pend_base, pend_res);
-            pend_base = ~0ull;
-        }
-        if (persist)
-            load_desc(u_next);
-    };
-    // receive verify: the u8 statuses, and the u16 L4 sums when asked for
-    const __amdgpu_buffer_rsrc_t l4_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        a.l4_out, static_cast<short>(0), static_cast<int>((XO && RX && a.l4_out) ? 2u * a.n : 0u), 0x00020000);
-    uint32_t pend_l4 = 0;
-    uint64_t pend_l4_base = ~0ull;
-    auto xo_store = [&](bool real) {
-        const uint64_t p = pend_base + lane;
-        const bool ok = real && pend_base != ~0ull && p < a.n;
-        if constexpr (RX)
-            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(pend_res[0]), out_rsrc,
-                                                 ok ? static_cast<uint32_t>(p) : kOobOffset, 0,
-                                                 RNS_STREAM_RX_NTSTORE ? kNtAux : 0);
-        else
-            __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(pend_res[0]), out_rsrc,
-                                                  ok ? static_cast<uint32_t>(2 * p) : kOobOffset, 0,
-                                                  RNS_STREAM_OUT == 1 ? kNtAux : 0);
-        if (real)
-            pend_base = ~0ull;
-    };
-    auto xo_store_l4 = [&]() {  // receive verify: the L4 sums (a null l4_out: 0 records, dropped)
-        const uint64_t p = pend_l4_base + lane;
-        const bool ok = pend_l4_base != ~0ull && p < a.n;
-        __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(pend_l4), l4_rsrc,
-                                              ok ? static_cast<uint32_t>(2 * p) : kOobOffset, 0, 0);
-        pend_l4_base = ~0ull;
-    };
-    // XO: extra operation j of the first row block (j < 4), a dropped store otherwise
-    auto xo_op = [&](int j, bool first_block, uint64_t u_next) {
-        const uint64_t ub = u_next < nunit ? u_next : nunit - 1;
-        const uint64_t pp = ub * kNP + lane;
-        const uint64_t q = pp < a.n ? pp : a.n - 1;
-        if (!first_block || j > 3) {
-            xo_store(false);
-        } else if (j == 0) {
-            xo_store(true);
-        } else if (j == 1) {
-            nx_r0 = a.blk_off[((ub * kNP) >> 6) + zero_v];
-        } else if (j == 2) {
-            nx_len[0] = static_cast<uint32_t>(a.len16[q]);  // (zeroed past the end at the unit's start)
-        } else if constexpr (RX) {
-            xo_store_l4();
-        } else {
-            if (a.seed)
-                nx_seed[0] = static_cast<uint32_t>(a.seed[q]);
-            else
-                xo_store(false);
-        }
-    };
-
-    for (uint64_t u = blockIdx.x; u < nunit; u += gridDim.x) {
-        const uint64_t base = u * kNP;
-        // (the lane intrinsics return int: widen through uint32_t, or an offset past 2 GiB sign-extends)
-        const uint64_t r0 =
-            ((static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nx_r0 >> 32))))
-              << 32) |
-             static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nx_r0)))) +
-            a.base_adjust;  // the wave's first packet
-        uint32_t len[KS], seed[KS], excl[KS];
-        uint32_t total = 0;  // the region's bytes (a multiple of 16 on the stream path)
+        };
+        // (issue order pinned: the loop consumes v[0] first, so its load must be the oldest
+        // on entry as on the back edge, or the compiler waits for all of them)
 #pragma unroll
-        for (int i = 0; i < KS; ++i) {
-            const bool in = base + 64u * i + lane < a.n;
-            len[i] = (!XO || in) ? nx_len[i] : 0u;
-            seed[i] = (!XO || (in && a.seed)) ? nx_seed[i] : 0u;
+        for (int j = 0; j < kStreamD; ++j) {
+            issue(j, v[j]);
+            __builtin_amdgcn_sched_barrier(0);
         }
-#pragma unroll
-        for (int i = 0; i < KS; ++i) {
-            const uint32_t pad = (len[i] + a.align_mask) & ~a.align_mask;
-            const uint32_t incl = wave_incl_scan(pad);
-            excl[i] = total + incl - pad;
-            total += __builtin_amdgcn_readlane(incl, 63);
-        }
-        uint32_t mine[KS];
-        bool odd = false;
-#pragma unroll
-        for (int i = 0; i < KS; ++i)
-            mine[i] = 0;
-
-        if ((r0 & 15) == 0) {
-            // ---- stream path ----
-            const uint32_t nrows = (total + 1023) >> 10;
-            tab[lane] = 0xFFFFFFFFu;                                          // tag 0x7FFF: never a row
-            wave_lds_fence();
-            uint32_t carry = 0;
-            uint4 v[kStreamD];
-            auto issue = [&](uint32_t k, uint4 &dst) {  // row k: chunk 64k + lane of the region
-                const uint64_t off = r0 + (static_cast<uint64_t>(k) << 10) + (lane << 4);
-                const bool in = k < nrows && off + 16 <= recs;
-                if constexpr (BUF) {
-                    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(
-                        rsrc, in ? static_cast<uint32_t>(off) : kOobOffset, 0, NT ? kNtAux : 0);
-                    dst = make_uint4(x.x, x.y, x.z, x.w);
-                } else {
-                    const uint4 x = load_chunk<NT>(a.arena + (in ? off : 0));
-                    dst = in ? x : make_uint4(0, 0, 0, 0);
-                }
-            };
-            // (issue order pinned: the loop consumes v[0] first, so its load must be the oldest
-            // on entry as on the back edge, or the compiler waits for all of them)
+        const uint32_t c0 = excl >> 4;
+        const uint32_t e = (excl + len - 1) >> 4;
+        const uint32_t ent = (lane << 4) | ((len - 1) & 15u);
+        const bool ne = len != 0;
+        for (uint32_t k0 = 0; k0 < nrows; k0 += kStreamD) {
 #pragma unroll
             for (int j = 0; j < kStreamD; ++j) {
-                issue(j, v[j]);
+                const uint32_t k = k0 + j;
+                const uint32_t tag = k << kTagShift;
+                // owners publish at the lanes that load their chunks in row k: the first chunk
+                // (padding chunks between packets, align_log2 > 4, belong to no packet, so a
+                // packet's sum is its end prefix minus its own start prefix), the last chunk
+                // (its valid bytes) and, receive verify, the first 4 chunks (the stash)
+#pragma unroll
+                for (uint32_t h = 0; h < 4; ++h) {
+                    const uint32_t c = c0 + h;
+                    if (ne && c <= e && (c >> 6) == k)
+                        tab[c & 63] = tag | kHead | (h << 14) | (h == 0 ? kStart : 0u) | (c == e ? kEnd : 0u) | ent;
+                }
+                if (ne && e >= c0 + 4 && (e >> 6) == k)
+                    tab[e & 63] = tag | kEnd | ent;
+                wave_lds_fence();
+                const uint32_t t = tab[lane];
+                const bool mark = (t >> kTagShift) == k;
+                const bool is_end = mark && (t & kEnd);
+                const uint32_t pk = (t >> 4) & 0xFFu;
+                uint4 x = v[j];
+                if (__ballot(is_end && (t & 15u) != 15u))  // a partial end chunk in this row
+                    x = keep_first(x, is_end ? (t & 15u) + 1u : 16u);
+                if (mark && (t & kHead))
+                    stash[pk * kNS + ((t >> 14) & 3u)] = x;
+                uint32_t s = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
+                s = __builtin_amdgcn_sad_u16(x.y, 0, s);
+                s = __builtin_amdgcn_sad_u16(x.z, 0, s);
+                s = __builtin_amdgcn_sad_u16(x.w, 0, s);
+                // the row D ahead into the registers this row just freed (past the region: no
+                // memory traffic).  Issued only after the row is consumed, so the loop-carried
+                // registers need no copy — a copy at the back edge waits for every load in flight.
                 __builtin_amdgcn_sched_barrier(0);
-                if constexpr (XO) {
-                    xo_store(false);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            if constexpr (!XO) {
-                overlap_point(u + gridDim.x);
+                issue(k + kStreamD, v[j]);
                 __builtin_amdgcn_sched_barrier(0);
-            }
-            for (uint32_t k0 = 0; k0 < nrows; k0 += kStreamD) {
-#pragma unroll
-                for (int j = 0; j < kStreamD; ++j) {
-                    const uint32_t k = k0 + j;
-                    const uint32_t tag = k << kTagShift;
-                    // owners publish at the lanes that load their chunks in row k: the first chunk
-                    // (padding chunks between packets, align_log2 > 4, belong to no packet, so a
-                    // packet's sum is its end prefix minus its own start prefix), the last chunk
-                    // (its valid bytes) and, receive verify, the first 4 chunks (the stash)
-#pragma unroll
-                    for (int i = 0; i < KS; ++i) {
-                        const uint32_t c0 = excl[i] >> 4;
-                        const uint32_t e = (excl[i] + len[i] - 1) >> 4;
-                        const uint32_t ent = ((64u * i + lane) << 4) | ((len[i] - 1) & 15u);
-                        const bool ne = len[i] != 0;
-                        if constexpr (RX) {
-#pragma unroll
-                            for (uint32_t h = 0; h < 4; ++h) {
-                                const uint32_t c = c0 + h;
-                                if (ne && c <= e && (c >> 6) == k)
-                                    tab[c & 63] = tag | kHead | (h << 14) | (h == 0 ? kStart : 0u) |
-                                                  (c == e ? kEnd : 0u) | ent;
-                            }
-                            if (ne && e >= c0 + 4 && (e >> 6) == k)
-                                tab[e & 63] = tag | kEnd | ent;
-                        } else {
-                            if (ne && (c0 >> 6) == k)
-                                tab[c0 & 63] = tag | kStart | (c0 == e ? kEnd : 0u) | ent;
-                            if (ne && e != c0 && (e >> 6) == k)
-                                tab[e & 63] = tag | kEnd | ent;
-                        }
-                    }
-                    wave_lds_fence();
-                    const uint32_t t = tab[lane];
-                    const bool mark = (t >> kTagShift) == k;
-                    const bool is_end = mark && (t & kEnd);
-                    const uint32_t pk = (t >> 4) & 0xFFu;
-                    uint4 x = v[j];
-                    if (__ballot(is_end && (t & 15u) != 15u))  // a partial end chunk in this row
-                        x = keep_first(x, is_end ? (t & 15u) + 1u : 16u);
-                    if constexpr (RX) {
-                        if (mark && (t & kHead))
-                            stash[pk * kNS + ((t >> 14) & 3u)] = x;
-                    }
-                    uint32_t s = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
-                    s = __builtin_amdgcn_sad_u16(x.y, 0, s);
-                    s = __builtin_amdgcn_sad_u16(x.z, 0, s);
-                    s = __builtin_amdgcn_sad_u16(x.w, 0, s);
-                    // the row D ahead into the registers this row just freed (past the region: no
-                    // memory traffic).  Issued only after the row is consumed, so the loop-carried
-                    // registers need no copy — a copy at the back edge waits for every load in flight.
-                    __builtin_amdgcn_sched_barrier(0);
-                    issue(k + kStreamD, v[j]);
-                    __builtin_amdgcn_sched_barrier(0);
-                    if constexpr (XO) {
-                        xo_op(j, k0 == 0, u + gridDim.x);
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-                    const uint32_t inc = wave_incl_scan(s);
-                    if (mark && (t & kStart))
-                        pstart[pk] = carry + inc - s;
-                    if (is_end)
-                        pend[pk] = carry + inc;
-                    carry += __builtin_amdgcn_readlane(inc, 63);
-                    wave_lds_fence();
-                }
-            }
-            if constexpr (XO) {
-                if (nrows == 0) {  // no row steps: the extra operations now
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        xo_op(j, true, u + gridDim.x);
-                }
-            }
-            // a packet's sum: the region prefix through its last chunk minus the prefix before its
-            // first (u32 differences: exact, a packet's LE sum is < 2^32)
-#pragma unroll
-            for (int i = 0; i < KS; ++i)
-                mine[i] = len[i] ? pend[64u * i + lane] - pstart[64u * i + lane] : 0u;
-        } else {
-            // ---- unaligned region (rare): the whole wave sums one packet at a time ----
-            if constexpr (XO) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    xo_op(j, true, u + gridDim.x);
-            } else {
-                overlap_point(u + gridDim.x);
-            }
-#pragma unroll
-            for (int i = 0; i < KS; ++i) {
-                const uint64_t start = r0 + excl[i];
-                const bool ok = start <= a.arena_bytes && len[i] <= a.arena_bytes - start;
-                uint64_t todo = __ballot(len[i] != 0 && ok);
-                while (todo) {
-                    const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
-                    todo &= todo - 1;
-                    const uint64_t st =
-                        (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start >> 32), o)))
-                         << 32) |
-                        static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start), o));
-                    const uint32_t L = __builtin_amdgcn_readlane(len[i], o);
-                    const Pkt k = make_pkt(st, L);
-                    uint32_t acc = 0;
-                    for (uint32_t cc = 0; cc < k.nch; cc += 64) {
-                        uint4 w[1];
-                        issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, w);
-                        mask_edges<64, 1, 1>(k, cc + lane, w);
-                        if constexpr (RX) {
-                            if (cc == 0 && lane < static_cast<uint32_t>(kNS))
-                                stash[(64u * i + o) * kNS + lane] = lane < k.nch ? w[0] : make_uint4(0, 0, 0, 0);
-                        }
-                        acc = sum_le<1, 1>(w, acc);
-                    }
-                    const uint32_t sum = group_allreduce<64>(acc);
-                    mine[i] = lane == o ? sum : mine[i];
-                }
-            }
-            odd = r0 & 1;  // every packet of the range shares the region start's misalignment
-        }
-        wave_lds_fence();
-#pragma unroll
-        for (int i = 0; i < KS; ++i) {
-            const uint64_t p = base + 64u * i + lane;
-            const bool live = p < a.n;
-            const uint64_t start = r0 + excl[i];
-            const bool ok = start <= a.arena_bytes && len[i] <= a.arena_bytes - start;
-            if constexpr (RX) {
-                uint32_t l4_res = 0;
-                const uint8_t stv = rx_finish<kNS>(a, stash + (64u * i + lane) * kNS, mine[i],
-                                                   static_cast<uint32_t>(start & 15), len[i], odd, false,
-                                                   live && ok && len[i] != 0, l4_res);
-                if constexpr (XO) {  // stored after the next unit's first rows
-                    pend_res[0] = stv;
-                    pend_l4 = l4_res;
-                } else if (live) {
-                    if constexpr (RNS_STREAM_RX_NTSTORE != 0)
-                        __builtin_nontemporal_store(stv, a.status + p);
-                    else
-                        a.status[p] = stv;
-                    if (a.l4_out)
-                        a.l4_out[p] = static_cast<uint16_t>(l4_res);
-                }
-            } else {
-                pend_res[i] = finalize_bits(mine[i], odd, false, seed[i], ok, a.flags);
-                if (a.bad) {
-                    const uint64_t rejected = __ballot(live && !ok);
-                    if (rejected && lane == 0)
-                        atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
-                }
+                const uint32_t inc = wave_incl_scan(s);
+                if (mark && (t & kStart))
+                    pstart[pk] = carry + inc - s;
+                if (is_end)
+                    pend[pk] = carry + inc;
+                carry += __builtin_amdgcn_readlane(inc, 63);
+                wave_lds_fence();
             }
         }
-        if constexpr (!RX || XO)
-            pend_base = base;
-        if constexpr (RX && XO)
-            pend_l4_base = base;
-        wave_lds_fence();  // the next range rewrites tab / pend / stash
+        // a packet's sum: the region prefix through its last chunk minus the prefix before its
+        // first (u32 differences: exact, a packet's LE sum is < 2^32)
+        mine = len ? pend[lane] - pstart[lane] : 0u;
+    } else {
+        // ---- unaligned region (rare): the whole wave sums one packet at a time ----
+        const uint64_t start = r0 + excl;
+        const bool ok = start <= a.arena_bytes && len <= a.arena_bytes - start;
+        uint64_t todo = __ballot(len != 0 && ok);
+        while (todo) {
+            const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
+            todo &= todo - 1;
+            const uint64_t st =
+                (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start >> 32), o)))
+                 << 32) |
+                static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start), o));
+            const uint32_t L = __builtin_amdgcn_readlane(len, o);
+            const Pkt k = make_pkt(st, L);
+            uint32_t acc = 0;
+            for (uint32_t cc = 0; cc < k.nch; cc += 64) {
+                uint4 w[1];
+                issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, w);
+                mask_edges<64, 1, 1>(k, cc + lane, w);
+                if (cc == 0 && lane < static_cast<uint32_t>(kNS))
+                    stash[o * kNS + lane] = lane < k.nch ? w[0] : make_uint4(0, 0, 0, 0);
+                acc = sum_le<1, 1>(w, acc);
+            }
+            const uint32_t sum = group_allreduce<64>(acc);
+            mine = lane == o ? sum : mine;
+        }
+        odd = r0 & 1;  // every packet of the range shares the region start's misalignment
     }
-    if constexpr (XO) {
-        xo_store(true);
-        if constexpr (RX)
-            xo_store_l4();
-    } else if constexpr (!RX) {
-        if (pend_base != ~0ull)
-            store_results(pend_base, pend_res);
+    wave_lds_fence();
+    const uint64_t start = r0 + excl;
+    const bool ok = start <= a.arena_bytes && len <= a.arena_bytes - start;
+    uint32_t l4_res = 0;
+    const uint8_t stv = rx_finish<kNS>(a, stash + lane * kNS, mine, static_cast<uint32_t>(start & 15), len, odd, false,
+                                       live && ok && len != 0, l4_res);
+    if (live) {
+        a.status[p] = stv;
+        if (a.l4_out)
+            a.l4_out[p] = static_cast<uint16_t>(l4_res);
     }
 }
 
 // ---------------------------------------------------------------------------
-// Fragment chains in rounds (util.rs:112-119 over NetBuffer fragments, buf.rs:466-487):
-// the form for NetBuffer-sized fragments (typical length >= 384 B).  A wave owns 64
-// consecutive packets; their fragments (the CSR range) are taken up to kChainFB at a time,
-// descriptors parked in LDS.  Each half-wave (32 lanes) sums one fragment per round, one
-// 16-byte chunk per lane — a fragment of up to 496 bytes at any start is one round, longer
-// ones take ceil(chunks/32) rounds — with D rounds in flight, fragments j = g, g+2, ... for
-// half g.  The half's 32 chunk sums reduce with DPP (row_shr 1-8, row_bcast:15) into lanes
-// 31 / 63; the fragment's LE word sum (exact: <= 128 KiB) is folded and byte-order corrected
-// by the fragment's start parity (RFC 1071 §2(B)) into the reference's per-fragment BE sum
-// mod 0xffff, parked in LDS, and each packet's owner lane folds its fragments in order as
-// util.rs:114-116 does.  A sub-batch holding a fragment past 128 KiB (the reference's u32
-// can wrap) sums its fragments one at a time with the exact big-endian path instead.
+// Row stream with owner captures (round 4; the packed form's plain checksum for
+// 16-byte-aligned packets of a typical length 113-1200 B: IMIX).
+//
+// A wave owns 64 consecutive packets and streams their bytes as ONE region, row k =
+// the region's k-th KiB (64 lanes x 16 B), D rows in flight — as csum_stream_kernel,
+// without its per-row LDS table.  The loading lanes know nothing about packets: each
+// sums its whole chunk (4 v_sad_u16), and one DPP scan per row gives the region's
+// inclusive prefix P at every chunk.  Packet p (chunks c0..e, 16-aligned start) needs
+// only two of those prefixes and its own end chunk:
+//     sum_p = P(e - 1) - P(c0 - 1) + (the first ((len - 1) & 15) + 1 bytes of chunk e)
+// (P(-1) = 0; e == c0: the end chunk alone).  The owner lane pulls P(c0 - 1) and
+// P(e - 1) from the lanes that hold them with ds_bpermute in the rows they fall in, and
+// loads its end chunk itself once per unit (issued before the rows: the line is then
+// an L2 hit for the row that streams it), so the end chunk's padding bytes never need a
+// per-row mask.  Per KiB: 4 sad + the scan + two captures, no LDS memory, no fences
+// (csum_stream_kernel: a table publish, two wave fences, the masks; 57 VALU/KB).
+// u32 differences are exact: a packet's LE word sum is < 2^32.
 // ---------------------------------------------------------------------------
-#ifndef RNS_CHAIN_FB
-#define RNS_CHAIN_FB 128
+#ifndef RNS_ROWS_OCC
+#define RNS_ROWS_OCC 8
 #endif
-#ifndef RNS_CHAIN_RD  // rounds in flight
-#define RNS_CHAIN_RD 4
+#ifndef RNS_ROWS_D  // rows (1 KiB loads) in flight per wave
+#define RNS_ROWS_D 4
 #endif
-#ifndef RNS_CHAIN_ROUNDS_OCC
-#define RNS_CHAIN_ROUNDS_OCC 8
-#endif
-constexpr uint32_t kChainFB = RNS_CHAIN_FB;
-constexpr int kChainRD = RNS_CHAIN_RD;
-
+constexpr int kRowsD = RNS_ROWS_D;
 template <bool NT, bool BUF>
-__global__ __launch_bounds__(64, RNS_CHAIN_ROUNDS_OCC) void csum_chain_rounds_kernel(const CsumArgs a)
+__global__ __launch_bounds__(64, RNS_ROWS_OCC) void csum_rows_kernel(const CsumArgs a)
 {
-    __shared__ uint4 finfo[kChainFB];    // per fragment: aligned start (lo, hi), length, [3:0] start & 15
-    __shared__ uint32_t fsum[kChainFB];  // per fragment: the BE sum (folded unless big)
-    __shared__ uint32_t fflag[kChainFB]; // per fragment: 1 = big (exact u32 sum), 2 = outside the arena
     const uint32_t lane = threadIdx.x;
-    const uint32_t half = lane >> 5, hl = lane & 31;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
     const uint64_t recs = buf_records(a);
-    constexpr uint32_t kBad = 0x80000000u;
-
     const uint64_t base = static_cast<uint64_t>(blockIdx.x) * 64;
     const uint64_t p = base + lane;
     const bool live = p < a.n;
-    uint32_t f0 = live ? a.first[p] : 0u, f1 = live ? a.first[p + 1] : 0u;
-    const bool rng_ok = f0 <= f1 && f1 <= a.n_frags;
-    if (!rng_ok)
-        f0 = f1 = 0;
-    uint32_t acc = ((a.seed && live) ? static_cast<uint32_t>(a.seed[p]) : 0u) | (rng_ok ? 0u : kBad);  // util.rs:113
-    const uint32_t F0 = wave_min_u32(f0 < f1 ? f0 : 0xFFFFFFFFu);
-    const uint32_t F1 = wave_max_u32(f0 < f1 ? f1 : 0u);
-    for (uint64_t fb = F0; fb < F1; fb += kChainFB) {
-        const uint32_t nf = static_cast<uint32_t>(min(static_cast<uint64_t>(kChainFB), F1 - fb));
-        // ---- the sub-batch's descriptors into LDS ----
-        bool any_big = false;
-#pragma unroll
-        for (uint32_t q = 0; q < kChainFB / 64; ++q) {
-            const uint32_t j = 64 * q + lane;
-            if (j < nf) {
-                const uint64_t foff = a.off[fb + j] + a.base_adjust;
-                const uint32_t flen = a.len[fb + j];
-                const bool fok = foff <= a.arena_bytes && flen <= a.arena_bytes - foff;
-                const uint32_t L = fok ? flen : 0u;
-                const uint64_t st = fok ? foff : 0;
-                finfo[j] = make_uint4(static_cast<uint32_t>(st & ~15ull), static_cast<uint32_t>(st >> 32), L,
-                                      static_cast<uint32_t>(st & 15));
-                fsum[j] = 0;
-                fflag[j] = (fok ? 0u : 2u) | (L > kNoWrapBytes ? 1u : 0u);
-                any_big = any_big || L > kNoWrapBytes;
+    const uint64_t q = live ? p : a.n - 1;  // branch-free descriptor loads
+    // (the block offset is loaded per lane at an index the compiler cannot prove uniform:
+    // a uniform load goes to SGPRs with a vmcnt(0) wait right away)
+    const uint32_t zero_v = __builtin_amdgcn_mbcnt_lo(0u, 0u);
+    const uint64_t r0v = a.blk_off[(base >> 6) + zero_v];
+    const uint32_t len = live ? static_cast<uint32_t>(a.len16[q]) : 0u;
+    const uint32_t seed = (a.seed && live) ? static_cast<uint32_t>(a.seed[q]) : 0u;
+    const uint64_t r0 =
+        ((static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(r0v >> 32))))
+          << 32) |
+         static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(r0v)))) +
+        a.base_adjust;  // the wave's first packet
+    const uint32_t pad = (len + a.align_mask) & ~a.align_mask;
+    const uint32_t incl = wave_incl_scan(pad);
+    const uint32_t excl = incl - pad;
+    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);  // the region's bytes
+    uint32_t mine = 0;
+    bool odd = false;
+    if ((r0 & 15) == 0) {
+        const uint32_t nrows = (total + 1023) >> 10;
+        const uint32_t c0 = excl >> 4;
+        const uint32_t e = len ? (excl + len - 1) >> 4 : c0;
+        // the end chunk, first: its line is then an L2 hit for the row that streams it
+        uint4 endv;
+        {
+            const uint64_t off = r0 + (static_cast<uint64_t>(e) << 4);
+            const bool in = len != 0 && off + 16 <= recs;
+            if constexpr (BUF) {
+                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, in ? static_cast<uint32_t>(off) : kOobOffset,
+                                                                      0, 0);
+                endv = make_uint4(x.x, x.y, x.z, x.w);
+            } else {
+                const uint4 x = load_chunk<false>(a.arena + (in ? off : 0));
+                endv = in ? x : make_uint4(0, 0, 0, 0);
             }
         }
-        wave_lds_fence();
-        if (!__ballot(any_big)) {
-            // ---- rounds: half g sums fragments g, g+2, ... one 32-chunk pass per round ----
-            // cursors (identical within a half): the issue cursor runs D rounds ahead of consumption
-            uint32_t ij = half, ip = 0;  // issue: fragment, pass
-            uint32_t lacc = 0;           // the consumed fragment's LE sum so far
-            uint4 v[kChainRD];
-            uint32_t inf[kChainRD];      // [0] valid, [1] last pass, [2] odd start, [10:3] fragment, [14:11] lo, [19:15] hi
-            auto issue = [&](uint4 &dst, uint32_t &info) {
-                uint64_t off = recs;  // past the arena: no load
-                info = 0;
-                if (ij < nf) {
-                    const uint4 fi = finfo[ij];
-                    const uint32_t nch = fi.z ? (fi.w + fi.z + 15) >> 4 : 0u;
-                    const uint32_t passes = max(1u, (nch + 31) >> 5);
-                    const uint32_t c = ip * 32 + hl;
-                    const uint32_t lo = c == 0 ? fi.w : 0u;
-                    const uint32_t hi = c + 1 == nch ? ((fi.w + fi.z - 1) & 15u) + 1u : 16u;
-                    if (c < nch)
-                        off = ((static_cast<uint64_t>(fi.y) << 32) | fi.x) + (static_cast<uint64_t>(c) << 4);
-                    info = 1u | (ip + 1 == passes ? 2u : 0u) | ((fi.w & 1u) << 2) | (ij << 3) | (lo << 11) |
-                           ((c < nch ? hi : 16u) << 15);
-                    if (++ip == passes) {
-                        ip = 0;
-                        ij += 2;
-                    }
-                }
-                const bool in = off + 16 <= recs;
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t vlane = lane << 4;
+        uint4 v[kRowsD];
+        auto issue = [&](uint32_t k, uint4 &dst) {  // row k: chunk 64k + lane of the region
+            if constexpr (BUF) {
+                // wave-uniform row base (a row past the region: out of range, no traffic)
+                const uint32_t sb = k < nrows ? static_cast<uint32_t>(r0) + (k << 10) : kOobOffset;
+                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, sb + vlane, 0, NT ? kNtAux : 0);
+                dst = make_uint4(x.x, x.y, x.z, x.w);
+            } else {
+                const uint64_t off = r0 + (static_cast<uint64_t>(k) << 10) + vlane;
+                const bool in = k < nrows && off + 16 <= recs;
+                const uint4 x = load_chunk<NT>(a.arena + (in ? off : 0));
+                dst = in ? x : make_uint4(0, 0, 0, 0);
+            }
+        };
+#pragma unroll
+        for (int j = 0; j < kRowsD; ++j) {
+            issue(j, v[j]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // the owner's partial end chunk (its padding bytes never count)
+        uint32_t part = 0;
+        if (len) {
+            const uint4 x = keep_first(endv, ((len - 1) & 15u) + 1u);
+            part = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
+            part = __builtin_amdgcn_sad_u16(x.y, 0, part);
+            part = __builtin_amdgcn_sad_u16(x.z, 0, part);
+            part = __builtin_amdgcn_sad_u16(x.w, 0, part);
+        }
+        // capture points: P(c0 - 1) and P(e - 1) (row, source lane); e == c0 takes the
+        // start's point twice (the difference is 0), c0 == 0 never captures (P(-1) = 0)
+        const uint32_t ca = c0 - 1u;
+        const uint32_t cb = e > c0 ? e - 1u : ca;
+        const uint32_t row_a = c0 ? ca >> 6 : 0xFFFFFFFFu, row_b = (e > c0 || c0) ? cb >> 6 : 0xFFFFFFFFu;
+        const int src_a = static_cast<int>((ca & 63u) << 2), src_b = static_cast<int>((cb & 63u) << 2);
+        uint32_t pa = 0, pb = 0, carry = 0;
+        for (uint32_t k0 = 0; k0 < nrows; k0 += kRowsD) {
+#pragma unroll
+            for (int j = 0; j < kRowsD; ++j) {
+                const uint32_t k = k0 + j;
+                const uint4 x = v[j];
+                uint32_t s = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
+                s = __builtin_amdgcn_sad_u16(x.y, 0, s);
+                s = __builtin_amdgcn_sad_u16(x.z, 0, s);
+                s = __builtin_amdgcn_sad_u16(x.w, 0, s);
+                // the row D ahead into the registers this row just freed (issued after the row
+                // is consumed: no loop-carried copy, exact vmcnt(D-1) waits)
+                __builtin_amdgcn_sched_barrier(0);
+                issue(k + kRowsD, v[j]);
+                __builtin_amdgcn_sched_barrier(0);
+                const uint32_t inc = wave_incl_scan(s);
+                const uint32_t ta = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_a, static_cast<int>(inc)));
+                const uint32_t tb = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_b, static_cast<int>(inc)));
+                pa = row_a == k ? carry + ta : pa;
+                pb = row_b == k ? carry + tb : pb;
+                carry += __builtin_amdgcn_readlane(inc, 63);
+            }
+        }
+        mine = len ? pb - pa + part : 0u;
+    } else {
+        // ---- unaligned region (rare): the whole wave sums one packet at a time ----
+        const uint64_t start = r0 + excl;
+        const bool ok = start <= a.arena_bytes && len <= a.arena_bytes - start;
+        uint64_t todo = __ballot(len != 0 && ok);
+        while (todo) {
+            const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
+            todo &= todo - 1;
+            const uint64_t st =
+                (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start >> 32), o)))
+                 << 32) |
+                static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start), o));
+            const uint32_t L = __builtin_amdgcn_readlane(len, o);
+            const Pkt k = make_pkt(st, L);
+            uint32_t acc = 0;
+            for (uint32_t cc = 0; cc < k.nch; cc += 64) {
+                uint4 w[1];
+                issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, w);
+                mask_edges<64, 1, 1>(k, cc + lane, w);
+                acc = sum_le<1, 1>(w, acc);
+            }
+            const uint32_t sum = group_allreduce<64>(acc);
+            mine = lane == o ? sum : mine;
+        }
+        odd = r0 & 1;  // every packet of the range shares the region start's misalignment
+    }
+    const uint64_t start = r0 + excl;
+    const bool ok = start <= a.arena_bytes && len <= a.arena_bytes - start;
+    const uint16_t res = finalize_bits(mine, odd, false, seed, ok, a.flags);
+    if (live) {
+        if (a.n < (1u << 30)) {  // buffer store, sc0|sc1 (the stream kernel's measured best, r03o)
+            const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+                static_cast<void *>(a.out), static_cast<short>(0), static_cast<int>(2u * a.n), 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b16(res, out_rsrc, static_cast<uint32_t>(2 * p), 0, RNS_STREAM_OUT_AUX);
+        } else {
+            __builtin_nontemporal_store(res, a.out + p);
+        }
+    }
+    if (a.bad) {
+        const uint64_t rejected = __ballot(live && !ok);
+        if (rejected && lane == 0)
+            atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Receive verify over the row stream (round 4; rns_rx_verify_packed_dev).  The sums come
+// from csum_rows_kernel's row stream and captures; the header (rx_finish reads the
+// datagram's first 64 bytes) comes from the owner's own loads of its first 4 chunks,
+// issued with its end chunk before the rows (L2 hits for the rows that stream them).
+// A unit whose datagrams all fit their 4 head chunks (ACK-sized datagrams) needs no
+// rows at all: each owner sums its own chunks.  Datagrams are masked to their length,
+// so rx_finish sees zeros past the end, as with the stash.
+// ---------------------------------------------------------------------------
+#ifndef RNS_RX_ROWS  // 1 = rns_rx_verify_packed_dev runs rx_rows_kernel for ACK-sized datagrams
+#define RNS_RX_ROWS 1
+#endif
+#ifndef RNS_RX_ROWS_OCC
+#define RNS_RX_ROWS_OCC 6
+#endif
+// Chunk i (i < 4) of a 16-byte-aligned datagram of len bytes at byte offset off: its bytes,
+// zero past the datagram's end (no load for a chunk wholly past it).
+template <bool BUF>
+__device__ __forceinline__ uint4 own_chunk(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint64_t recs, uint64_t off,
+                                           uint32_t len, uint32_t i)
+{
+    const uint64_t o = off + 16u * i;
+    const bool in = 16u * i < len && o + 16 <= recs;
+    uint4 x;
+    if constexpr (BUF) {
+        const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rsrc, in ? static_cast<uint32_t>(o) : kOobOffset, 0, 0);
+        x = make_uint4(y.x, y.y, y.z, y.w);
+    } else {
+        const uint4 y = load_chunk<false>(a.arena + (in ? o : 0));
+        x = in ? y : make_uint4(0, 0, 0, 0);
+    }
+    return x;
+}
+
+template <bool NT, bool BUF>
+__global__ __launch_bounds__(64, RNS_RX_ROWS_OCC) void rx_rows_kernel(const CsumArgs a)
+{
+    const uint32_t lane = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
+    const uint64_t recs = buf_records(a);
+    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * 64;
+    const uint64_t p = base + lane;
+    const bool live = p < a.n;
+    const uint64_t q = live ? p : a.n - 1;
+    const uint32_t zero_v = __builtin_amdgcn_mbcnt_lo(0u, 0u);
+    const uint64_t r0v = a.blk_off[(base >> 6) + zero_v];
+    const uint32_t len = live ? static_cast<uint32_t>(a.len16[q]) : 0u;
+    const uint64_t r0 =
+        ((static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(r0v >> 32))))
+          << 32) |
+         static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(r0v)))) +
+        a.base_adjust;
+    const uint32_t pad = (len + a.align_mask) & ~a.align_mask;
+    const uint32_t incl = wave_incl_scan(pad);
+    const uint32_t excl = incl - pad;
+    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+    const uint64_t start = r0 + excl;
+    const bool ok = start <= a.arena_bytes && len <= a.arena_bytes - start;
+    uint32_t mine = 0;
+    bool odd = false;
+    uint4 own[5];
+    if ((r0 & 15) == 0) {
+        const uint32_t c0 = excl >> 4;
+        const uint32_t e = len ? (excl + len - 1) >> 4 : c0;
+        const bool longd = len > 64;  // chunks past the 4 head chunks: the row stream sums them
+        // the head chunks and (a long datagram) the end chunk, before any row
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            own[i] = own_chunk<BUF>(a, rsrc, recs, start, len, i);
+        own[4] = make_uint4(0, 0, 0, 0);
+        const uint4 endv = own_chunk<BUF>(a, rsrc, recs, r0 + (static_cast<uint64_t>(e) << 4), longd ? 16u : 0u, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t nv = ((len - 1) & 15u) + 1u;  // valid bytes of the end chunk
+        uint32_t part = 0;
+        if (__ballot(longd)) {
+            const uint32_t nrows = (total + 1023) >> 10;
+            const uint32_t vlane = lane << 4;
+            uint4 v[kRowsD];
+            auto issue = [&](uint32_t k, uint4 &dst) {
                 if constexpr (BUF) {
-                    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(
-                        rsrc, in ? static_cast<uint32_t>(off) : kOobOffset, 0, NT ? kNtAux : 0);
+                    const uint32_t sb = k < nrows ? static_cast<uint32_t>(r0) + (k << 10) : kOobOffset;
+                    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, sb + vlane, 0, NT ? kNtAux : 0);
                     dst = make_uint4(x.x, x.y, x.z, x.w);
                 } else {
+                    const uint64_t off = r0 + (static_cast<uint64_t>(k) << 10) + vlane;
+                    const bool in = k < nrows && off + 16 <= recs;
                     const uint4 x = load_chunk<NT>(a.arena + (in ? off : 0));
                     dst = in ? x : make_uint4(0, 0, 0, 0);
                 }
             };
 #pragma unroll
-            for (int r = 0; r < kChainRD; ++r) {
-                issue(v[r], inf[r]);
+            for (int j = 0; j < kRowsD; ++j) {
+                issue(j, v[j]);
                 __builtin_amdgcn_sched_barrier(0);
             }
-            while (__ballot(inf[0] & 1u)) {
+            if (longd) {
+                const uint4 x = keep_first(endv, nv);
+                part = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
+                part = __builtin_amdgcn_sad_u16(x.y, 0, part);
+                part = __builtin_amdgcn_sad_u16(x.z, 0, part);
+                part = __builtin_amdgcn_sad_u16(x.w, 0, part);
+            }
+            const uint32_t ca = c0 - 1u, cb = e - 1u;  // long datagrams only: e > c0
+            const uint32_t row_a = (longd && c0) ? ca >> 6 : 0xFFFFFFFFu, row_b = longd ? cb >> 6 : 0xFFFFFFFFu;
+            const int src_a = static_cast<int>((ca & 63u) << 2), src_b = static_cast<int>((cb & 63u) << 2);
+            uint32_t pa = 0, pb = 0, carry = 0;
+            for (uint32_t k0 = 0; k0 < nrows; k0 += kRowsD) {
 #pragma unroll
-                for (int r = 0; r < kChainRD; ++r) {
-                    const uint32_t in = inf[r];
-                    uint4 x = v[r];
-                    const uint32_t lo = (in >> 11) & 15u, hi = (in >> 15) & 31u;
-                    if (__ballot(lo != 0 || hi != 16)) {  // a fragment starts or ends inside a chunk here
-                        x.x = keep_bytes(x.x, static_cast<int>(lo), static_cast<int>(hi), 0);
-                        x.y = keep_bytes(x.y, static_cast<int>(lo), static_cast<int>(hi), 4);
-                        x.z = keep_bytes(x.z, static_cast<int>(lo), static_cast<int>(hi), 8);
-                        x.w = keep_bytes(x.w, static_cast<int>(lo), static_cast<int>(hi), 12);
-                    }
+                for (int j = 0; j < kRowsD; ++j) {
+                    const uint32_t k = k0 + j;
+                    const uint4 x = v[j];
                     uint32_t s = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
                     s = __builtin_amdgcn_sad_u16(x.y, 0, s);
                     s = __builtin_amdgcn_sad_u16(x.z, 0, s);
                     s = __builtin_amdgcn_sad_u16(x.w, 0, s);
                     __builtin_amdgcn_sched_barrier(0);
-                    issue(v[r], inf[r]);  // the round D ahead into the registers this round freed
+                    issue(k + kRowsD, v[j]);
                     __builtin_amdgcn_sched_barrier(0);
-                    // the half's 32 chunk sums: an inclusive scan within each half, totals in lanes 31 / 63
-                    uint32_t t = s;
-                    t += dpp_or_zero<0x111>(s);
-                    t += dpp_or_zero<0x112>(s);
-                    t += dpp_or_zero<0x113>(s);
-                    t += dpp_or_zero<0x114, 0xF, 0xE>(t);
-                    t += dpp_or_zero<0x118, 0xF, 0xC>(t);
-                    t += dpp_or_zero<0x142, 0xA, 0xF>(t);
-                    const uint32_t part = half ? __builtin_amdgcn_readlane(t, 63) : __builtin_amdgcn_readlane(t, 31);
-                    if (in & 1u) {
-                        lacc += part;
-                        if (in & 2u) {  // the fragment's last pass: fold, correct the byte order, park it
-                            const uint32_t xx = fold16(lacc);
-                            const uint32_t g = (in & 4u) ? xx : (((xx & 0xff) << 8) | (xx >> 8));
-                            if (hl == 0)
-                                fsum[(in >> 3) & 0xFFu] = g;
-                            lacc = 0;
-                        }
-                    }
+                    const uint32_t inc = wave_incl_scan(s);
+                    const uint32_t ta = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_a, static_cast<int>(inc)));
+                    const uint32_t tb = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_b, static_cast<int>(inc)));
+                    pa = row_a == k ? carry + ta : pa;
+                    pb = row_b == k ? carry + tb : pb;
+                    carry += __builtin_amdgcn_readlane(inc, 63);
                 }
             }
-        } else {
-            // ---- a fragment past 128 KiB in this sub-batch: one fragment at a time, exact ----
-            for (uint32_t j = 0; j < nf; ++j) {
-                const uint4 fi = finfo[j];
-                const uint64_t st = ((static_cast<uint64_t>(fi.y) << 32) | fi.x) + fi.w;
-                const uint32_t L = fi.z;
-                if (L == 0)
-                    continue;
-                const Pkt k = make_pkt(st, L);
-                uint32_t hs = 0, ls = 0, le = 0;
-                for (uint32_t cc = 0; cc < k.nch; cc += 64) {
-                    uint4 wv[1];
-                    issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, wv);
-                    mask_edges<64, 1, 1>(k, cc + lane, wv);
-                    if (k.big)
-                        sum_be<1, 1>(wv, (st & 1) ? 0x01000100u : 0x00010001u, hs, ls);
-                    else
-                        le = sum_le<1, 1>(wv, le);
-                }
-                const uint32_t sum = group_allreduce<64>(k.big ? (hs << 8) + ls : le);
-                uint32_t gv = sum;
-                if (!k.big) {
-                    const uint32_t xx = fold16(sum);
-                    gv = (st & 1) ? xx : (((xx & 0xff) << 8) | (xx >> 8));
-                }
-                if (lane == 0)
-                    fsum[j] = gv;
+            mine = longd ? pb - pa + part : 0u;
+        }
+        // short datagrams (<= 64 B): the sum of the head chunks, masked to the length
+        if (!longd && len) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint4 x = 16u * i + 16u > len ? keep_first(own[i], 16u * i < len ? len - 16u * i : 1u) : own[i];
+                const bool live_i = 16u * i < len;
+                uint32_t s = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
+                s = __builtin_amdgcn_sad_u16(x.y, 0, s);
+                s = __builtin_amdgcn_sad_u16(x.z, 0, s);
+                s = __builtin_amdgcn_sad_u16(x.w, 0, s);
+                mine += live_i ? s : 0u;
             }
         }
-        wave_lds_fence();
-        // owner lanes: each packet's fragments inside [fb, fb + nf), in order (util.rs:114-116)
-        const uint64_t t0 = max(static_cast<uint64_t>(f0), fb);
-        const uint64_t t1 = min(static_cast<uint64_t>(f1), fb + nf);
-        for (uint64_t t = t0; t < t1; ++t) {
-            const uint32_t gv = fsum[t - fb], fv = fflag[t - fb];
-            const uint32_t bad = (acc & kBad) | ((fv & 2u) ? kBad : 0u);
-            uint32_t sm = (acc & 0xffffu) + gv;  // big: util.rs:89-99 mod 2^32; else <= 0x1fffe
-            if (fv & 1u) {
-                while (sm > 0xffff)  // util.rs:101-103
-                    sm = (sm & 0xffff) + (sm >> 16);
-            } else {
-                sm = (sm & 0xffff) + (sm >> 16);  // one end-around step folds it
-            }
-            acc = sm | bad;
+        // mask the head chunks to the datagram (rx_finish sees zeros past its end)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (16u * i + 16u > len)
+                own[i] = 16u * i < len ? keep_first(own[i], len - 16u * i) : make_uint4(0, 0, 0, 0);
         }
-        wave_lds_fence();  // the next sub-batch rewrites finfo / fsum / fflag
+    } else {
+        // ---- unaligned region (rare): the whole wave sums one datagram at a time; each
+        // owner takes its 5 chunks from the 16-byte boundary below its start ----
+        uint64_t todo = __ballot(len != 0 && ok);
+        while (todo) {
+            const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
+            todo &= todo - 1;
+            const uint64_t st =
+                (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start >> 32), o)))
+                 << 32) |
+                static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start), o));
+            const uint32_t L = __builtin_amdgcn_readlane(len, o);
+            const Pkt k = make_pkt(st, L);
+            uint32_t acc = 0;
+            for (uint32_t cc = 0; cc < k.nch; cc += 64) {
+                uint4 w[1];
+                issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, w);
+                mask_edges<64, 1, 1>(k, cc + lane, w);
+                acc = sum_le<1, 1>(w, acc);
+            }
+            const uint32_t sum = group_allreduce<64>(acc);
+            mine = lane == o ? sum : mine;
+        }
+        odd = r0 & 1;
+        const uint64_t b0 = start & ~15ull;
+        const uint32_t s0 = static_cast<uint32_t>(start & 15);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            // bytes [s0, s0 + len) of the 80 from b0 (keep_bytes works per dword)
+            const uint4 y = own_chunk<BUF>(a, rsrc, recs, b0, (len && ok) ? s0 + len : 0u, i);
+            const int lo = static_cast<int>(s0) - 16 * i, hi = static_cast<int>(s0 + len) - 16 * i;
+            own[i] = make_uint4(keep_bytes(y.x, lo, hi, 0), keep_bytes(y.y, lo, hi, 4), keep_bytes(y.z, lo, hi, 8),
+                                keep_bytes(y.w, lo, hi, 12));
+        }
     }
-    uint32_t r = acc & 0xffffu;
-    if (a.flags & RNS_FLAG_COMPLEMENT)
-        r ^= 0xffff;
-    const bool ok = !(acc & kBad);
-    if (live)
-        a.out[p] = static_cast<uint16_t>(ok ? r : 0u);  // 64 consecutive u16: one 128-byte store
-    if (a.bad) {
-        const uint64_t rejected = __ballot(live && !ok);
-        if (rejected && lane == 0)
-            atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
+    uint32_t l4_res = 0;
+    const uint8_t stv = rx_finish<5>(a, own, mine, static_cast<uint32_t>(start & 15), len, odd, false,
+                                     live && ok && len != 0, l4_res);
+    if (live) {
+        a.status[p] = stv;
+        if (a.l4_out)
+            a.l4_out[p] = static_cast<uint16_t>(l4_res);
     }
 }
 
@@ -2743,73 +2686,14 @@ Shape pick_shape(uint32_t len_hint)
 // The packed form's kernels (separate instantiations, so the explicit-descriptor
 // kernels carry no packed-form code): the mixed kernel, or for tiny packets the
 // rounds kernel with pick_shape's G=4, U=1 shape.
-// Packed-form stream launch.  One 64-packet set per wave: 2 or 4 sets per wave (one row
-// stream over 128-256 packets) measured no faster on IMIX, 40-byte and 576-byte batches,
-// and slower where their descriptors spill (profiles/r03_stream_ab.json, session r03f).
-#ifndef RNS_STREAM_KS  // A/B knob: packet sets per wave
-#define RNS_STREAM_KS 1
-#endif
-// Compute units of the current device (256 on MI355X), cached per device.
-int device_cus()
+// Receive verify's stream launch: one wave per 64-datagram unit.
+int launch_stream_rx(const CsumArgs &a, hipStream_t st)
 {
-    static int cus[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
-        return 256;
-    if (cus[dev] == 0) {
-        int c = 0;
-        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
-            c = 256;
-        cus[dev] = c;
-    }
-    return cus[dev];
-}
-
-template <int MODE>
-int launch_stream(const CsumArgs &a, int ks, hipStream_t st)
-{
-    const bool buf = buf_records(a) < kOobOffset;
-    const uint64_t all_units = (static_cast<uint64_t>(a.n) + 64u * ks - 1) / (64u * ks);
-    uint64_t units = all_units;
-#ifndef RNS_STREAM_TINY_CAP  // A/B knob: grid cap (waves loop over units) for ACK-sized packets; 0 = none
-#define RNS_STREAM_TINY_CAP 0
-#endif
-#ifndef RNS_STREAM_PERSIST  // A/B knob: at most this many waves per SIMD (waves loop over units); 0 = none
-#define RNS_STREAM_PERSIST 0
-#endif
-#ifndef RNS_STREAM_XO  // A/B knob: capped grids run the extra-operation-per-row form (plain mode)
-#define RNS_STREAM_XO 1
-#endif
-    if (RNS_STREAM_TINY_CAP && a.arena_bytes / std::max<uint64_t>(a.n, 1) <= 128)
-        units = std::min<uint64_t>(units, RNS_STREAM_TINY_CAP);
-    if (RNS_STREAM_PERSIST)
-        units = std::min<uint64_t>(units, static_cast<uint64_t>(device_cus()) * 4u * RNS_STREAM_PERSIST);
-#ifndef RNS_STREAM_UPW  // A/B knob: units per wave (grid = units / UPW, the XO form when > 1); 1 = one-shot
-#define RNS_STREAM_UPW 1
-#endif
-    if (RNS_STREAM_UPW > 1)
-        units = (units + RNS_STREAM_UPW - 1) / RNS_STREAM_UPW;
-    const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(units, 0x7FFFFFFFu))), block(64);
-    constexpr bool NT = RNS_STREAM_NT != 0;
-#define RNS_LAUNCH_STREAM(K)                                                                       \
-    do {                                                                                           \
-        if (buf)                                                                                   \
-            hipLaunchKernelGGL((csum_stream_kernel<MODE, K, NT, true>), grid, block, 0, st, a);    \
-        else                                                                                       \
-            hipLaunchKernelGGL((csum_stream_kernel<MODE, K, NT, false>), grid, block, 0, st, a);   \
-    } while (0)
-    if constexpr (MODE == kStashNone && RNS_STREAM_KS > 1) {
-        (void)ks;
-        RNS_LAUNCH_STREAM(RNS_STREAM_KS);
-    } else if (RNS_STREAM_XO && buf && grid.x < all_units && a.n < (1u << 30)) {  // (result offsets below kOobOffset)
-        // a capped grid on the buffer path: the extra-operation-per-row form (delayed stores,
-        // next unit's descriptors in flight)
-        hipLaunchKernelGGL((csum_stream_kernel<MODE, 1, NT, true, true>), grid, block, 0, st, a);
-    } else {
-        (void)ks;  // (receive verify: always one set per wave — its stash is 5 chunks per datagram)
-        RNS_LAUNCH_STREAM(1);
-    }
-#undef RNS_LAUNCH_STREAM
+    const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);
+    if (buf_records(a) < kOobOffset)
+        hipLaunchKernelGGL((csum_stream_kernel<RNS_STREAM_NT != 0, true>), grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL((csum_stream_kernel<RNS_STREAM_NT != 0, false>), grid, block, 0, st, a);
     return hip_status(hipGetLastError());
 }
 
@@ -2828,8 +2712,14 @@ int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
 #define RNS_STREAM_TINY 0
 #endif
     if (RNS_STREAM && a.align_mask >= 15u && (!tiny || RNS_STREAM_TINY) &&
-        (a.len_hint == 0 || a.len_hint <= RNS_STREAM_MAXLEN))
-        return launch_stream<kStashNone>(a, 1, st);
+        (a.len_hint == 0 || a.len_hint <= RNS_STREAM_MAXLEN)) {
+        const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);
+        if (buf)
+            hipLaunchKernelGGL((csum_rows_kernel<RNS_STREAM_NT != 0, true>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_rows_kernel<RNS_STREAM_NT != 0, false>), grid, block, 0, st, a);
+        return hip_status(hipGetLastError());
+    }
     const uint64_t batches = (static_cast<uint64_t>(a.n) + 63) / 64;  // one wave per 64 packets
     const uint64_t wpb = ((sh.variant & 4u) ? kMixedBlock<false> : kBlock) / 64;  // waves per workgroup
     uint64_t blocks = (batches + wpb - 1) / wpb;
@@ -3107,21 +2997,6 @@ int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
     const bool buf = buf_records(a) < kOobOffset;
     // RNS_FLAG_CHAIN_RUNS: the run-checking kernel (buffer path; a hint, ignored otherwise)
     const bool runs = kChainRuns && (flags & RNS_FLAG_CHAIN_RUNS) && buf;
-#ifndef RNS_CHAIN_ROUNDS  // A/B knob: 0 = never the rounds kernel (measured slower on c3 layouts, r03l);
-#define RNS_CHAIN_ROUNDS 0   // 1 = for NetBuffer-sized fragments; 2 = also with the runs hint
-#endif
-    if (RNS_CHAIN_ROUNDS && (frag_len_hint ? frag_len_hint : 512u) >= 384u && (!runs || RNS_CHAIN_ROUNDS == 2)) {
-        const dim3 rgrid(static_cast<uint32_t>((static_cast<uint64_t>(n_pkts) + 63) / 64)), rblock(64);
-        if (nt && buf)
-            hipLaunchKernelGGL((csum_chain_rounds_kernel<true, true>), rgrid, rblock, 0, st, a);
-        else if (nt)
-            hipLaunchKernelGGL((csum_chain_rounds_kernel<true, false>), rgrid, rblock, 0, st, a);
-        else if (buf)
-            hipLaunchKernelGGL((csum_chain_rounds_kernel<false, true>), rgrid, rblock, 0, st, a);
-        else
-            hipLaunchKernelGGL((csum_chain_rounds_kernel<false, false>), rgrid, rblock, 0, st, a);
-        return hip_status(hipGetLastError());
-    }
 #define RNS_CHAIN_LAUNCH(KM)                                                                      \
     if (runs && nt)                                                                               \
         hipLaunchKernelGGL((csum_chain_kernel<true, true, KM, true>), grid, block, 0, st, a);     \
@@ -3263,7 +3138,19 @@ int rns_rx_verify_packed_dev(const uint8_t *d_arena, uint64_t arena_bytes, const
     a.l4_out = d_l4_sum;
     a.local4_sum = be_sum(local_ipv4, 4);
     a.local6_sum = be_sum(local_ipv6, 16);
-    return launch_stream<kStashHead>(a, 1, static_cast<hipStream_t>(stream));
+    // ACK-sized datagrams (arena bytes per datagram <= 128): the row-stream form, whose owners
+    // take their datagrams whole (64 B: 13.3 -> 12.1 us per step, session r04b); larger ones
+    // the stream kernel's stash (IMIX verify 478 vs 496 us with rx_rows_kernel).
+    if (RNS_RX_ROWS && a.arena_bytes / n <= 128) {
+        const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(n) + 63) / 64)), block(64);
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        if (buf_records(a) < kOobOffset)
+            hipLaunchKernelGGL((rx_rows_kernel<RNS_STREAM_NT != 0, true>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((rx_rows_kernel<RNS_STREAM_NT != 0, false>), grid, block, 0, st, a);
+        return hip_status(hipGetLastError());
+    }
+    return launch_stream_rx(a, static_cast<hipStream_t>(stream));
 }
 
 int rns_tx_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off, const uint32_t *d_len,
@@ -3605,11 +3492,12 @@ const char *rns_csum_shape_name(uint32_t len_hint)
 
 const char *rns_build_info(void)
 {
-    return "rns_checksum abi=1 offload-arch=gfx950 kernels=csum_stream_kernel (packed form: 1 KiB rows per "
-           "64-packet region, prefix sums per packet; plain and receive-verify modes), csum_mixed_kernel (per-wave "
-           "size-class sort; verify / fill / transmit-finalize stash modes), csum_rounds_kernel, csum_batch_kernel, "
-           "csum_chain_kernel (one pass, per-fragment fold) (v_sad_u16 LE sums, v_dot4 BE sums past 128 KiB, wave64, "
-           "DPP reductions)";
+    return "rns_checksum abi=1 offload-arch=gfx950 kernels=csum_rows_kernel (packed form: 1 KiB rows per 64-packet "
+           "region, owners capture two region prefixes and sum their own end chunk), rx_rows_kernel (its receive-verify "
+           "form for ACK-sized datagrams), csum_stream_kernel (receive verify with an LDS stash), csum_mixed_kernel "
+           "(per-wave size-class sort; verify / fill / transmit-finalize stash modes), csum_rounds_kernel, "
+           "csum_batch_kernel, csum_chain_kernel (one pass, per-fragment fold) (v_sad_u16 LE sums, v_dot4 BE sums past "
+           "128 KiB, wave64, DPP reductions)";
 }
 
 int rns_device_count(void)

@@ -98,7 +98,7 @@ def test_two_rank_gloo_bench_main(tmp_path, oracle, config, n, launch):
     (no WORLD_SIZE), where bench.py must start the two ranks itself."""
     script = tmp_path / "worker.py"
     script.write_text(WORKER.format(root=ROOT, n=n, config=config, outdir=str(tmp_path)))
-    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env = dict(os.environ, OMP_NUM_THREADS="1", RNS_BENCH_BACKEND="gloo")  # CPU ranks, also on a GPU host
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     if launch == "torchrun":
@@ -236,7 +236,7 @@ def test_two_rank_gloo_verify_allreduce(tmp_path, config, n):
     (one per rank) equals the corruptions planted over the whole (sharded) batch."""
     script = tmp_path / "worker.py"
     script.write_text(VERIFY_WORKER.format(root=ROOT, n=n, config=config, outdir=str(tmp_path)))
-    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env = dict(os.environ, OMP_NUM_THREADS="1", RNS_BENCH_BACKEND="gloo")  # CPU ranks, also on a GPU host
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(script)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
@@ -273,7 +273,7 @@ def test_gpus_disagreeing_with_world_size_fails(tmp_path):
 
 
 def test_gpus_zero_rejected(tmp_path):
-    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env = dict(os.environ, OMP_NUM_THREADS="1", RNS_BENCH_BACKEND="gloo")  # CPU ranks, also on a GPU host
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "0", "--steps", "1"],
                        capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))

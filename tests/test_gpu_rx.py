@@ -252,3 +252,26 @@ def test_packed_full_size_equals_descriptor_entry(name):
     assert int(((got & _lib.RNS_RX_ACCEPT) == 0).sum().item()) == b.expected_bad
     del b
     torch.cuda.empty_cache()
+
+
+def test_output_buffers_are_checked():
+    """The kernels write one status (and L4 sum) per datagram: an undersized or wrongly typed
+    output buffer, or descriptors on another device, is refused before any launch."""
+    from rustnetworkstack_amd.batch import rx_verify_packed
+    arena = torch.zeros(4096, dtype=torch.uint8, device=DEV)
+    off = torch.arange(0, 4096, 64, dtype=torch.int64, device=DEV)
+    ln = torch.full((64,), 64, dtype=torch.int32, device=DEV)
+    with pytest.raises(ValueError):
+        rx_verify(arena, off, ln, L4, L6, status=torch.empty(63, dtype=torch.uint8, device=DEV))
+    with pytest.raises(ValueError):
+        rx_verify(arena, off, ln, L4, L6, l4_sum=torch.empty(10, dtype=torch.int16, device=DEV))
+    with pytest.raises(TypeError):
+        rx_verify(arena, off, ln, L4, L6, status=torch.empty(64, dtype=torch.int16, device=DEV))
+    blk = torch.zeros(1, dtype=torch.int64, device=DEV)
+    len16 = torch.full((64,), 64, dtype=torch.int16, device=DEV)
+    with pytest.raises(ValueError):
+        rx_verify_packed(arena, blk, len16, L4, L6, status=torch.empty(1, dtype=torch.uint8, device=DEV))
+    with pytest.raises(ValueError):
+        rx_verify_packed(arena, blk, len16, L4, L6, l4_sum=torch.empty(63, dtype=torch.uint16, device=DEV))
+    st = rx_verify_packed(arena, blk, len16, L4, L6, status=torch.empty(64, dtype=torch.uint8, device=DEV))
+    assert st.numel() == 64

@@ -13,7 +13,7 @@ Timing: one pair of HIP events around K back-to-back launches on the launch stre
 median of R rounds.  GB/s counts algorithmic bytes (payload read + result bytes
 written); descriptor and workspace traffic is not credited.
 
-    python tools/bench_ops.py [--steps 20] [--rounds 5] [--out profiles/r01_ops.json]
+    python tools/bench_ops.py [--steps 20] [--rounds 5] [--out profiles/archive/r01/r01_ops.json]
 """
 import argparse
 import json

@@ -3,7 +3,7 @@ value per dispatch, with the gfx950 corrections of MI355X_MICROARCH.md §HBM
 (FETCH_SIZE KiB x 2 for wide streaming reads; WRITE_SIZE KiB as is) and the
 EA write requests in bytes (TCC_EA0_WRREQ counts 32-byte requests unless _64B).
 
-    python tools/pmc_write.py gpurun_out/<tag> [--out profiles/r03_pmc_write.json]
+    python tools/pmc_write.py gpurun_out/<tag> [--out profiles/archive/r03/r03_pmc_write.json]
 """
 import argparse
 import csv

@@ -8,7 +8,7 @@ On the GPU box (tools/gpu_session.sh does this):
 then here (or there):
 
     python tools/profile_bench.py --trace <dir>/run_kernel_trace.csv --bench bench.log \\
-        --out profiles/r02_rocprof_bench_c3_1500B.json
+        --out profiles/archive/r02/r02_rocprof_bench_c3_1500B.json
 
 bench.py's own dispatches of the product kernel come first, in order: W warmup
 launches, K timed launches (one event pair around all of them), then, with
