@@ -508,10 +508,8 @@ class GpuEngine:
         from rustnetworkstack_amd import _lib
         if self.op == "verify":
             if self.verify_packed:
-                if self.layout.n and self.layout.arena_bytes // self.layout.n <= 128:  # the library's ACK-sized rule
-                    return ("rx_rows_kernel (rns_rx_verify_packed_dev, ACK-sized datagrams: owners load their "
-                            "datagrams whole)")
-                return "csum_stream_kernel<RX> (rns_rx_verify_packed_dev: 1 KiB rows + header stash)"
+                return ("csum_stream_kernel<RX> (rns_rx_verify_packed_dev: 1 KiB rows + header stash; units of "
+                        "ACK-sized datagrams: owners load their datagrams whole)")
             return "csum_mixed_kernel<RX> (rns_rx_verify_dev: class-sorted data pass + header stash)"
         mean = self.layout.mean_len
         if self.packed and self.layout.n and int(self.layout.off[0]) % 16 == 0 and 112 < mean <= 1200:

@@ -38,12 +38,6 @@
 
 #include "rns_checksum.h"
 
-// Diagnostic A/B builds leave work out on purpose (wrong results) to measure what it costs.
-// They must never be mistaken for the product: each needs RNS_DIAGNOSTIC_BUILD as well.
-#if (defined(RNS_DIAG_NOSEED) || defined(RNS_FILL_NOSTORE)) && !defined(RNS_DIAGNOSTIC_BUILD)
-#error "RNS_DIAG_NOSEED and RNS_FILL_NOSTORE give wrong results: add -DRNS_DIAGNOSTIC_BUILD"
-#endif
-
 namespace {
 
 #ifndef RNS_BLOCK
@@ -365,19 +359,7 @@ struct Pkt {
     bool big;             // > kNoWrapBytes: exact big-endian path
     int stash_lo;         // stash: first chunk to copy to LDS
     int stash_at;         // stash: LDS chunk index of that chunk's slot
-    uint32_t len;         // in-round fill (RNS_FILL_INROUND): the packet's length,
-    uint32_t aux;         //   its checksum field offset
-    uint32_t seed;        //   and its seed
 };
-
-// A/B knob: transmit fill stores each packet's field from the group that summed it,
-// in the same round (the block's lines were just read), instead of from the owner
-// lane after the wave's 64 packets.
-#ifdef RNS_FILL_INROUND
-constexpr bool kFillInRound = true;
-#else
-constexpr bool kFillInRound = false;
-#endif
 
 __device__ __forceinline__ Pkt make_pkt(uint64_t start, uint32_t L)
 {
@@ -390,9 +372,6 @@ __device__ __forceinline__ Pkt make_pkt(uint64_t start, uint32_t L)
     k.big = L > kNoWrapBytes;
     k.stash_lo = 0;
     k.stash_at = 0;
-    k.len = L;
-    k.aux = 0xFFFFFFFFu;
-    k.seed = 0;
     return k;
 }
 
@@ -414,7 +393,7 @@ __device__ __forceinline__ void set_stash(Pkt &k, uint32_t slot, uint32_t field,
 
 template <int G, int MODE = kStashNone>
 __device__ __forceinline__ Pkt fetch_pkt(uint64_t d_start, uint32_t d_len, uint32_t src, uint32_t d_aux = 0xFFFFFFFFu,
-                                         uint32_t apar = 0, uint32_t d_seed = 0)
+                                         uint32_t apar = 0)
 {
     const uint32_t lo = bcast_from<G>(static_cast<uint32_t>(d_start), src);
     const uint32_t hi = bcast_from<G>(static_cast<uint32_t>(d_start >> 32), src);
@@ -422,10 +401,6 @@ __device__ __forceinline__ Pkt fetch_pkt(uint64_t d_start, uint32_t d_len, uint3
     const uint32_t x = MODE == kStashField ? bcast_from<G>(d_aux, src) : 0xFFFFFFFFu;
     Pkt k = make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L);
     set_stash<MODE>(k, src, x, apar);
-    if constexpr (MODE == kStashField && kFillInRound) {
-        k.aux = x;
-        k.seed = bcast_from<G>(d_seed, src);
-    }
     return k;
 }
 
@@ -778,7 +753,7 @@ constexpr int kUMax = umax_of();  // chunk slots of the widest class
 template <bool NT, bool BUF, int MODE>
 __device__ __forceinline__ Pkt prefetch_class(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint32_t n,
                                               const ClassRun (&cr)[kNumClasses], uint64_t s_start, uint32_t s_len,
-                                              uint32_t s_aux, uint32_t lane, uint4 (&w)[kUMax], uint32_t s_seed = 0)
+                                              uint32_t s_aux, uint32_t lane, uint4 (&w)[kUMax])
 {
     uint32_t lg = 6, U = 0, off = 0, cnt = 0;
 #pragma unroll
@@ -800,10 +775,6 @@ __device__ __forceinline__ Pkt prefetch_class(const CsumArgs &a, __amdgpu_buffer
     const uint32_t x = MODE == kStashField ? static_cast<uint32_t>(__shfl(static_cast<int>(s_aux), src, 64)) : 0xFFFFFFFFu;
     Pkt k = make_pkt((static_cast<uint64_t>(hi) << 32) | lo, L);
     set_stash<MODE>(k, static_cast<uint32_t>(src), x, arena_parity(a));
-    if constexpr (MODE == kStashField && kFillInRound) {
-        k.aux = x;
-        k.seed = static_cast<uint32_t>(__shfl(static_cast<int>(s_seed), src, 64));
-    }
     k.nch = valid ? k.nch : 0u;
     const uint64_t first = k.start - static_cast<uint64_t>(k.s);
 #pragma unroll
@@ -877,7 +848,6 @@ __device__ __forceinline__ void store_block(uint4 *p, uint4 v)
 __device__ __forceinline__ void fill_store(const CsumArgs &a, const FillSite &f, uint64_t d_start, uint32_t d_field,
                                            uint16_t res, const uint4 *stp)
 {
-#ifndef RNS_FILL_NOSTORE
     uint8_t *arena_w = const_cast<uint8_t *>(a.arena);
     const uint32_t be = (res >> 8) | ((res & 0xffu) << 8);
     if (f.w_size) {
@@ -907,9 +877,6 @@ __device__ __forceinline__ void fill_store(const CsumArgs &a, const FillSite &f,
         q[0] = static_cast<uint8_t>(res >> 8);
         q[1] = static_cast<uint8_t>(res);
     }
-#else
-    (void)a; (void)f; (void)d_start; (void)d_field; (void)res; (void)stp;
-#endif
 }
 
 // All rounds of class C.  On entry (cur, v) hold round 0's prefetched first pass;
@@ -918,8 +885,7 @@ template <uint32_t C, bool NT, bool BUF, int MODE>
 __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc,
                                           const ClassRun (&cr)[kNumClasses], uint32_t next, uint64_t s_start,
                                           uint32_t s_len, uint32_t s_aux, bool in_class, uint32_t rank,
-                                          uint32_t lane, Pkt &cur, uint4 (&v)[kUMax], uint32_t &mine, uint4 *st,
-                                          uint32_t s_seed)
+                                          uint32_t lane, Pkt &cur, uint4 (&v)[kUMax], uint32_t &mine, uint4 *st)
 {
     constexpr int G = 1 << kClassLog2G[C];
     constexpr int U = static_cast<int>(kClassU[C]);
@@ -931,26 +897,12 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
         return;  // (cur, v) already hold the next class's prefetch
     auto fetch = [&](uint32_t r) {  // group `grp` of round r: sorted position off + r*P + grp
         const uint32_t i = r * P + grp;
-        Pkt k = fetch_pkt<G, MODE>(s_start, s_len, cr[C].off + (i < cr[C].cnt ? i : 0), s_aux, arena_parity(a),
-                                   s_seed);
+        Pkt k = fetch_pkt<G, MODE>(s_start, s_len, cr[C].off + (i < cr[C].cnt ? i : 0), s_aux, arena_parity(a));
         k.nch = (i < cr[C].cnt) ? k.nch : 0u;
         return k;
     };
     auto finish = [&](uint32_t r) {  // consume round r from (cur, v), route each sum to its owner lane
-        uint32_t words = group_allreduce<G>(packet_partial<G, U, NT, BUF, kUMax, MODE>(a, rsrc, cur, sub, v, st));
-        if constexpr (MODE == kStashField && kFillInRound) {
-            // the group finishes its packet now, while the field's lines were just read:
-            // words -> the complemented result, stored into the field by lane 0 of the group
-            wave_lds_fence();  // the stash was written by this group's lanes
-            const bool ok = cur.nch != 0;  // a rejected packet was given length 0
-            const uint4 *stp = st + cur.stash_at;
-            const FillSite f = fill_site(a, cur.start, cur.len, cur.aux, cur.big,
-                                         reinterpret_cast<const uint8_t *>(stp), ok);
-            const uint16_t res = finalize_bits(words - f.contrib, cur.start & 1, cur.big, cur.seed, ok, a.flags);
-            if (ok && sub == 0)
-                fill_store(a, f, cur.start, cur.aux, res, stp);
-            words = res;
-        }
+        const uint32_t words = group_allreduce<G>(packet_partial<G, U, NT, BUF, kUMax, MODE>(a, rsrc, cur, sub, v, st));
         if constexpr (G == 64) {
             mine = (in_class && rank == r) ? words : mine;  // wave-uniform sum
         } else {
@@ -970,7 +922,7 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
             v[u] = w[u];
     }
     uint4 w[kUMax];
-    const Pkt nxt = prefetch_class<NT, BUF, MODE>(a, rsrc, next, cr, s_start, s_len, s_aux, lane, w, s_seed);
+    const Pkt nxt = prefetch_class<NT, BUF, MODE>(a, rsrc, next, cr, s_start, s_len, s_aux, lane, w);
     finish(rounds - 1);
     cur = nxt;
 #pragma unroll
@@ -986,11 +938,8 @@ __device__ __forceinline__ void run_class(const CsumArgs &a, __amdgpu_buffer_rsr
 // its group; lane 4g + q keeps slot q's sum, and each owner lane pulls its packet's
 // with one shuffle.  Issues its own round 0 (it is always the first class) and, like
 // run_class, leaves the next class's first pass in flight in (cur, v).
-#ifndef RNS_TINY_Q
-#define RNS_TINY_Q 4
-#endif
-constexpr uint32_t kTinyQ = kFillInRound ? 1u : RNS_TINY_Q;  // 1: class 0 runs G4/U1 through run_class
-static_assert(kTinyQ == 1 || (kTinyQ == 4 && kClassLog2G[0] == 2 && kClassMax[0] <= 4), "tiny class shape");
+constexpr uint32_t kTinyQ = 4;
+static_assert(kClassLog2G[0] == 2 && kClassMax[0] <= 4, "tiny class shape");
 
 template <bool NT, bool BUF, int MODE>
 __device__ __forceinline__ void run_tiny(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc,
@@ -1065,7 +1014,7 @@ __device__ __forceinline__ void run_tiny(const CsumArgs &a, __amdgpu_buffer_rsrc
 template <bool NT, bool BUF, int MODE, bool TINY = (kTinyQ > 1)>
 __device__ __forceinline__ uint32_t wave_class_pass(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint64_t d_start,
                                                     uint32_t d_len, uint32_t d_aux, uint32_t lane, uint4 *st,
-                                                    uint32_t &pos, uint32_t d_seed = 0)
+                                                    uint32_t &pos)
 {
     // size class of this lane's packet (kNumClasses: empty, no rounds at all — e.g. the
     // fragments the chain kernel merged into their run's first); ranks within the
@@ -1113,19 +1062,17 @@ __device__ __forceinline__ uint32_t wave_class_pass(const CsumArgs &a, __amdgpu_
     const uint64_t s_start = (static_cast<uint64_t>(s_hi) << 32) | s_lo;
     const uint32_t s_aux = MODE == kStashField
         ? static_cast<uint32_t>(__builtin_amdgcn_ds_permute(addr, static_cast<int>(d_aux))) : 0u;
-    const uint32_t s_seed = (MODE == kStashField && kFillInRound)
-        ? static_cast<uint32_t>(__builtin_amdgcn_ds_permute(addr, static_cast<int>(d_seed))) : 0u;
 
     uint32_t mine = 0;
     uint4 v[kUMax];
     Pkt cur;
 #define RNS_RUN_CLASS(C)                                                                                  \
     run_class<C, NT, BUF, MODE>(a, rsrc, cr, next[C + 1], s_start, s_len, s_aux, cls == C, rank, lane, \
-                                cur, v, mine, st, s_seed)
+                                cur, v, mine, st)
     if (TINY && cr[0].cnt) {  // the tiny class issues its own first round
         run_tiny<NT, BUF, MODE>(a, rsrc, cr, next[1], s_start, s_len, s_aux, cls == 0, rank, lane, cur, v, mine, st);
     } else {
-        cur = prefetch_class<NT, BUF, MODE>(a, rsrc, next[0], cr, s_start, s_len, s_aux, lane, v, s_seed);
+        cur = prefetch_class<NT, BUF, MODE>(a, rsrc, next[0], cr, s_start, s_len, s_aux, lane, v);
         if (!TINY)
             RNS_RUN_CLASS(0);
     }
@@ -1153,12 +1100,8 @@ __device__ __forceinline__ uint32_t wave_class_pass(const CsumArgs &a, __amdgpu_
 // trimmed packet pairs them.  The L4 seed is the pseudo-header sum with dest = the
 // LOCAL address, as the reference passes netif::get_ipaddr().
 // ---------------------------------------------------------------------------
-// A/B knob: receive verify's owner-lane finish takes a short path for 16-byte-aligned
-// datagrams (header dwords as stashed; a 20-byte IPv4 header summed without byte masks).
-#ifndef RNS_RX_ALIGNED_FAST
-#define RNS_RX_ALIGNED_FAST 1
-#endif
-constexpr bool kRxAlignedFast = RNS_RX_ALIGNED_FAST != 0;
+// Receive verify's owner-lane finish takes a short path for 16-byte-aligned datagrams
+// (header dwords as stashed; a 20-byte IPv4 header summed without byte masks).
 
 enum : uint32_t {
     kMetaV4 = 1, kMetaV6 = 2, kMetaFrag = 4, kMetaMalformed = 8,
@@ -1318,7 +1261,7 @@ __device__ __forceinline__ uint8_t rx_finish(const CsumArgs &a, const uint4 *own
     for (int i = 0; i < 3; ++i)
         ch[i] = own[i];
     uint32_t head[6];
-    if (kRxAlignedFast && s == 0) {  // 16-byte-aligned datagram: the dwords as they are
+    if (s == 0) {  // 16-byte-aligned datagram: the dwords as they are
         const uint32_t w6[6] = {ch[0].x, ch[0].y, ch[0].z, ch[0].w, ch[1].x, ch[1].y};
 #pragma unroll
         for (int k = 0; k < 6; ++k)
@@ -1332,7 +1275,7 @@ __device__ __forceinline__ uint8_t rx_finish(const CsumArgs &a, const uint4 *own
     if (!(rp.meta & kMetaMalformed)) {
         const int hlo = static_cast<int>(s), hhi = hlo + static_cast<int>(rp.hdr);  // <= 15 + 60
         uint32_t H;
-        if (kRxAlignedFast && hlo == 0 && hhi == 20) {  // aligned IPv4 header, no options: 5 dwords
+        if (hlo == 0 && hhi == 20) {  // aligned IPv4 header, no options: 5 dwords
             H = __builtin_amdgcn_sad_u16(ch[0].x, 0, 0u);
             H = __builtin_amdgcn_sad_u16(ch[0].y, 0, H);
             H = __builtin_amdgcn_sad_u16(ch[0].z, 0, H);
@@ -1409,11 +1352,6 @@ __device__ __forceinline__ Desc<BUF> load_desc(const CsumArgs &a, uint64_t p)
 #endif
 template <bool STASH>
 constexpr int kMixedBlock = STASH ? 64 : RNS_MIXED_PLAIN_BLOCK;
-// A/B knob: packed descriptors of the next wave batch loaded beside this batch's seeds.
-#ifndef RNS_MIXED_PACKED_PF
-#define RNS_MIXED_PACKED_PF 1
-#endif
-constexpr bool kMixedPackedPf = RNS_MIXED_PACKED_PF != 0;
 
 // FILL (transmit in-place fill, tcp.rs:957-973 / udp.rs:158-171 / icmp.rs:87-112 /
 // ip.rs:158-159): the checksum is that of the packet with its 2-byte field zeroed
@@ -1458,7 +1396,7 @@ csum_mixed_kernel(const CsumArgs a)
     // Packed form: the next wave batch's lengths (and block base) are loaded together
     // with this batch's seeds after the class pass — one memory latency between two
     // batches instead of two, and nothing extra is live during the class pass.
-    constexpr bool kPf = PACKED && kMixedPackedPf;
+    constexpr bool kPf = PACKED;  // packed: the next wave batch's lengths loaded beside this batch's seeds
     uint32_t nx_len = 0;
     uint64_t nx_blk = 0;
     auto load_next = [&](uint64_t b) {  // branch-free: past the end re-reads the last packet
@@ -1500,7 +1438,7 @@ csum_mixed_kernel(const CsumArgs a)
         }
         const bool odd = d_start & 1, big = d_len > kNoWrapBytes;  // all finalize needs of (start, len)
         uint32_t pos;
-        uint32_t mine = wave_class_pass<NT, BUF, kMode>(a, rsrc, d_start, d_len, d_field, lane, st, pos, d_seed);
+        uint32_t mine = wave_class_pass<NT, BUF, kMode>(a, rsrc, d_start, d_len, d_field, lane, st, pos);
 
         if constexpr (TX) {
             // Transmit finalize: mine = the whole datagram's word sum.  From the stash
@@ -1627,23 +1565,17 @@ csum_mixed_kernel(const CsumArgs a)
             continue;
         }
         FillSite fs{};
-        if constexpr (FILL && !kFillInRound) {  // take the field's bytes out of the sum: it counts as zero
+        if constexpr (FILL) {  // take the field's bytes out of the sum: it counts as zero
             wave_lds_fence();  // the stash was written by other lanes of this wave
             fs = fill_site(a, d_start, d_len, d_field, big, reinterpret_cast<const uint8_t *>(st + pos * kNS), d_ok);
             mine -= fs.contrib;
         }
         if constexpr (PACKED) {
-#ifndef RNS_DIAG_NOSEED  // diagnostic A/B only (wrong results): what the seed load's latency costs
             d_seed = (a.seed && live) ? a.seed[p] : 0u;
-#endif
             if constexpr (kPf)
                 load_next(base + wstep);  // in flight while this batch finishes and stores
         }
-        uint16_t res;
-        if constexpr (FILL && kFillInRound)
-            res = d_ok ? static_cast<uint16_t>(mine) : static_cast<uint16_t>(0);  // finished (and stored) in-round
-        else
-            res = finalize_bits(mine, odd, big, d_seed, d_ok, a.flags);
+        const uint16_t res = finalize_bits(mine, odd, big, d_seed, d_ok, a.flags);
 #ifndef RNS_MIXED_NTSTORE  // nontemporal result stores in the plain class kernel (c3 232.4 -> 229.5 us per step, r03l)
 #define RNS_MIXED_NTSTORE 1
 #endif
@@ -1653,7 +1585,7 @@ csum_mixed_kernel(const CsumArgs a)
             else
                 a.out[p] = res;  // 64 consecutive u16: one 128-byte store
         }
-        if constexpr (FILL && !kFillInRound) {
+        if constexpr (FILL) {
             if (live && d_ok)  // set_be16(&mut header[f..f+2], checksum), after the wave read its 64 packets
                 fill_store(a, fs, d_start, d_field, res, st + pos * kNS);
         }
@@ -1677,7 +1609,9 @@ csum_mixed_kernel(const CsumArgs a)
 //     iff both are zero);
 //   longer: sum = fold((sum + W) mod 2^32), W = the exact BE word sum mod 2^32 —
 //     the reference's wrapping u32 accumulator itself.
-// Exact for any fragment count and size; no scratch, no second kernel.
+// Exact for any fragment count and size; no second kernel.  At 4 waves/SIMD every
+// instantiation spills 8-44 B/lane (8 on the default path); 3 waves/SIMD spills nothing
+// and is 4-7 % slower on c3 chains (session r04b), so 4 stays (tools/scratch_report.sh).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
 {
@@ -1787,10 +1721,7 @@ __global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(
     uint32_t (&pk)[kPk][KMAX * 64] = pk_lds[threadIdx.x >> 6];
     // A wave stops looking for runs after a batch without them (the check costs a round
     // of descriptor loads): the fragment path is exact for every batch anyway.
-#ifndef RNS_CHAIN_TRY  // A/B knob: 0 = the run code compiled in but never tried
-#define RNS_CHAIN_TRY 1
-#endif
-    bool try_runs = RUNS && RNS_CHAIN_TRY;
+    bool try_runs = RUNS;
     const uint32_t wave = (blockIdx.x * kChainBlock + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * kChainBlock) >> 6;
     const uint32_t K = KMAX == 1 ? 1u : a.chain_k;
@@ -1985,12 +1916,33 @@ __device__ __forceinline__ uint4 keep_first(uint4 v, uint32_t c)
 // 454-461, sc0|sc1 455.9 (r03i, r03o; sc0 alone 474, sc1 457, sc1|nt 461-466, sc0|nt 459-460).
 constexpr int kStreamD = RNS_STREAM_D;
 
-// Receive verify (rns_rx_verify_packed_dev) of datagrams larger than ACKs: the lanes that
-// load a datagram's first 4 chunks (64 bytes: every IPv4 header incl. options, the IPv6
-// header) also copy them to an LDS stash, and the owner finishes exactly as the class
-// kernel's receive verify does (rx_finish).  (Round 3's plain mode of this kernel gave way
-// to csum_rows_kernel in round 4; forms that gave a wave several units were measured slower
-// in round 3 and removed.)  One wave per 64-datagram unit.
+// Chunk i of the datagram of len bytes whose 16-byte-aligned chunk 0 is at byte offset off
+// (zero, with no load, for a chunk wholly past the end; the last chunk is not masked).
+template <bool BUF>
+__device__ __forceinline__ uint4 own_chunk(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint64_t recs, uint64_t off,
+                                           uint32_t len, uint32_t i)
+{
+    const uint64_t o = off + 16u * i;
+    const bool in = 16u * i < len && o + 16 <= recs;
+    uint4 x;
+    if constexpr (BUF) {
+        const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rsrc, in ? static_cast<uint32_t>(o) : kOobOffset, 0, 0);
+        x = make_uint4(y.x, y.y, y.z, y.w);
+    } else {
+        const uint4 y = load_chunk<false>(a.arena + (in ? o : 0));
+        x = in ? y : make_uint4(0, 0, 0, 0);
+    }
+    return x;
+}
+
+// Receive verify (rns_rx_verify_packed_dev).  The lanes that load a datagram's first 4
+// chunks (64 bytes: every IPv4 header incl. options, the IPv6 header) also copy them to an
+// LDS stash, and the owner finishes exactly as the class kernel's receive verify does
+// (rx_finish).  A unit whose datagrams all fit 4 chunks (ACK-sized: 64 B TCP/IPv4 with
+// options) skips the rows: each owner loads its datagram whole and finishes from registers
+// (64 B datagrams: 13.3 -> 12.1 us per step, session r04b).  (Round 3's plain mode of this
+// kernel gave way to csum_rows_kernel in round 4; forms that gave a wave several units were
+// measured slower in round 3 and removed.)  One wave per 64-datagram unit.
 template <bool NT, bool BUF>
 __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(const CsumArgs a)
 {
@@ -2028,6 +1980,32 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
     uint32_t mine = 0;
     bool odd = false;
 
+    if ((r0 & 15) == 0 && !__ballot(len > 64)) {
+        // ---- ACK-sized unit: every owner takes its datagram whole ----
+        const uint64_t start = r0 + excl;
+        const bool ok = start <= a.arena_bytes && len <= a.arena_bytes - start;
+        uint4 own[5];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint4 x = own_chunk<BUF>(a, rsrc, recs, start, len, i);
+            if (16u * i + 16u > len)  // rx_finish sees zeros past the end, as from the stash
+                x = 16u * i < len ? keep_first(x, len - 16u * i) : make_uint4(0, 0, 0, 0);
+            own[i] = x;
+            mine = __builtin_amdgcn_sad_u16(x.x, 0, mine);
+            mine = __builtin_amdgcn_sad_u16(x.y, 0, mine);
+            mine = __builtin_amdgcn_sad_u16(x.z, 0, mine);
+            mine = __builtin_amdgcn_sad_u16(x.w, 0, mine);
+        }
+        own[4] = make_uint4(0, 0, 0, 0);
+        uint32_t l4_res = 0;
+        const uint8_t stv = rx_finish<kNS>(a, own, mine, 0u, len, false, false, live && ok && len != 0, l4_res);
+        if (live) {
+            a.status[p] = stv;
+            if (a.l4_out)
+                a.l4_out[p] = static_cast<uint16_t>(l4_res);
+        }
+        return;
+    }
     if ((r0 & 15) == 0) {
         // ---- stream path ----
         const uint32_t nrows = (total + 1023) >> 10;
@@ -2171,7 +2149,7 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
 #define RNS_ROWS_OCC 8
 #endif
 #ifndef RNS_ROWS_D  // rows (1 KiB loads) in flight per wave
-#define RNS_ROWS_D 4
+#define RNS_ROWS_D 8  // (c5 isolated 456 -> 451-453 us against 4, session r04c)
 #endif
 constexpr int kRowsD = RNS_ROWS_D;
 template <bool NT, bool BUF>
@@ -2322,199 +2300,6 @@ __global__ __launch_bounds__(64, RNS_ROWS_OCC) void csum_rows_kernel(const CsumA
         const uint64_t rejected = __ballot(live && !ok);
         if (rejected && lane == 0)
             atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Receive verify over the row stream (round 4; rns_rx_verify_packed_dev).  The sums come
-// from csum_rows_kernel's row stream and captures; the header (rx_finish reads the
-// datagram's first 64 bytes) comes from the owner's own loads of its first 4 chunks,
-// issued with its end chunk before the rows (L2 hits for the rows that stream them).
-// A unit whose datagrams all fit their 4 head chunks (ACK-sized datagrams) needs no
-// rows at all: each owner sums its own chunks.  Datagrams are masked to their length,
-// so rx_finish sees zeros past the end, as with the stash.
-// ---------------------------------------------------------------------------
-#ifndef RNS_RX_ROWS  // 1 = rns_rx_verify_packed_dev runs rx_rows_kernel for ACK-sized datagrams
-#define RNS_RX_ROWS 1
-#endif
-#ifndef RNS_RX_ROWS_OCC
-#define RNS_RX_ROWS_OCC 6
-#endif
-// Chunk i (i < 4) of a 16-byte-aligned datagram of len bytes at byte offset off: its bytes,
-// zero past the datagram's end (no load for a chunk wholly past it).
-template <bool BUF>
-__device__ __forceinline__ uint4 own_chunk(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint64_t recs, uint64_t off,
-                                           uint32_t len, uint32_t i)
-{
-    const uint64_t o = off + 16u * i;
-    const bool in = 16u * i < len && o + 16 <= recs;
-    uint4 x;
-    if constexpr (BUF) {
-        const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rsrc, in ? static_cast<uint32_t>(o) : kOobOffset, 0, 0);
-        x = make_uint4(y.x, y.y, y.z, y.w);
-    } else {
-        const uint4 y = load_chunk<false>(a.arena + (in ? o : 0));
-        x = in ? y : make_uint4(0, 0, 0, 0);
-    }
-    return x;
-}
-
-template <bool NT, bool BUF>
-__global__ __launch_bounds__(64, RNS_RX_ROWS_OCC) void rx_rows_kernel(const CsumArgs a)
-{
-    const uint32_t lane = threadIdx.x;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
-    const uint64_t recs = buf_records(a);
-    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * 64;
-    const uint64_t p = base + lane;
-    const bool live = p < a.n;
-    const uint64_t q = live ? p : a.n - 1;
-    const uint32_t zero_v = __builtin_amdgcn_mbcnt_lo(0u, 0u);
-    const uint64_t r0v = a.blk_off[(base >> 6) + zero_v];
-    const uint32_t len = live ? static_cast<uint32_t>(a.len16[q]) : 0u;
-    const uint64_t r0 =
-        ((static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(r0v >> 32))))
-          << 32) |
-         static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(r0v)))) +
-        a.base_adjust;
-    const uint32_t pad = (len + a.align_mask) & ~a.align_mask;
-    const uint32_t incl = wave_incl_scan(pad);
-    const uint32_t excl = incl - pad;
-    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-    const uint64_t start = r0 + excl;
-    const bool ok = start <= a.arena_bytes && len <= a.arena_bytes - start;
-    uint32_t mine = 0;
-    bool odd = false;
-    uint4 own[5];
-    if ((r0 & 15) == 0) {
-        const uint32_t c0 = excl >> 4;
-        const uint32_t e = len ? (excl + len - 1) >> 4 : c0;
-        const bool longd = len > 64;  // chunks past the 4 head chunks: the row stream sums them
-        // the head chunks and (a long datagram) the end chunk, before any row
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            own[i] = own_chunk<BUF>(a, rsrc, recs, start, len, i);
-        own[4] = make_uint4(0, 0, 0, 0);
-        const uint4 endv = own_chunk<BUF>(a, rsrc, recs, r0 + (static_cast<uint64_t>(e) << 4), longd ? 16u : 0u, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        const uint32_t nv = ((len - 1) & 15u) + 1u;  // valid bytes of the end chunk
-        uint32_t part = 0;
-        if (__ballot(longd)) {
-            const uint32_t nrows = (total + 1023) >> 10;
-            const uint32_t vlane = lane << 4;
-            uint4 v[kRowsD];
-            auto issue = [&](uint32_t k, uint4 &dst) {
-                if constexpr (BUF) {
-                    const uint32_t sb = k < nrows ? static_cast<uint32_t>(r0) + (k << 10) : kOobOffset;
-                    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, sb + vlane, 0, NT ? kNtAux : 0);
-                    dst = make_uint4(x.x, x.y, x.z, x.w);
-                } else {
-                    const uint64_t off = r0 + (static_cast<uint64_t>(k) << 10) + vlane;
-                    const bool in = k < nrows && off + 16 <= recs;
-                    const uint4 x = load_chunk<NT>(a.arena + (in ? off : 0));
-                    dst = in ? x : make_uint4(0, 0, 0, 0);
-                }
-            };
-#pragma unroll
-            for (int j = 0; j < kRowsD; ++j) {
-                issue(j, v[j]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            if (longd) {
-                const uint4 x = keep_first(endv, nv);
-                part = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
-                part = __builtin_amdgcn_sad_u16(x.y, 0, part);
-                part = __builtin_amdgcn_sad_u16(x.z, 0, part);
-                part = __builtin_amdgcn_sad_u16(x.w, 0, part);
-            }
-            const uint32_t ca = c0 - 1u, cb = e - 1u;  // long datagrams only: e > c0
-            const uint32_t row_a = (longd && c0) ? ca >> 6 : 0xFFFFFFFFu, row_b = longd ? cb >> 6 : 0xFFFFFFFFu;
-            const int src_a = static_cast<int>((ca & 63u) << 2), src_b = static_cast<int>((cb & 63u) << 2);
-            uint32_t pa = 0, pb = 0, carry = 0;
-            for (uint32_t k0 = 0; k0 < nrows; k0 += kRowsD) {
-#pragma unroll
-                for (int j = 0; j < kRowsD; ++j) {
-                    const uint32_t k = k0 + j;
-                    const uint4 x = v[j];
-                    uint32_t s = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
-                    s = __builtin_amdgcn_sad_u16(x.y, 0, s);
-                    s = __builtin_amdgcn_sad_u16(x.z, 0, s);
-                    s = __builtin_amdgcn_sad_u16(x.w, 0, s);
-                    __builtin_amdgcn_sched_barrier(0);
-                    issue(k + kRowsD, v[j]);
-                    __builtin_amdgcn_sched_barrier(0);
-                    const uint32_t inc = wave_incl_scan(s);
-                    const uint32_t ta = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_a, static_cast<int>(inc)));
-                    const uint32_t tb = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_b, static_cast<int>(inc)));
-                    pa = row_a == k ? carry + ta : pa;
-                    pb = row_b == k ? carry + tb : pb;
-                    carry += __builtin_amdgcn_readlane(inc, 63);
-                }
-            }
-            mine = longd ? pb - pa + part : 0u;
-        }
-        // short datagrams (<= 64 B): the sum of the head chunks, masked to the length
-        if (!longd && len) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint4 x = 16u * i + 16u > len ? keep_first(own[i], 16u * i < len ? len - 16u * i : 1u) : own[i];
-                const bool live_i = 16u * i < len;
-                uint32_t s = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
-                s = __builtin_amdgcn_sad_u16(x.y, 0, s);
-                s = __builtin_amdgcn_sad_u16(x.z, 0, s);
-                s = __builtin_amdgcn_sad_u16(x.w, 0, s);
-                mine += live_i ? s : 0u;
-            }
-        }
-        // mask the head chunks to the datagram (rx_finish sees zeros past its end)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (16u * i + 16u > len)
-                own[i] = 16u * i < len ? keep_first(own[i], len - 16u * i) : make_uint4(0, 0, 0, 0);
-        }
-    } else {
-        // ---- unaligned region (rare): the whole wave sums one datagram at a time; each
-        // owner takes its 5 chunks from the 16-byte boundary below its start ----
-        uint64_t todo = __ballot(len != 0 && ok);
-        while (todo) {
-            const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
-            todo &= todo - 1;
-            const uint64_t st =
-                (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start >> 32), o)))
-                 << 32) |
-                static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start), o));
-            const uint32_t L = __builtin_amdgcn_readlane(len, o);
-            const Pkt k = make_pkt(st, L);
-            uint32_t acc = 0;
-            for (uint32_t cc = 0; cc < k.nch; cc += 64) {
-                uint4 w[1];
-                issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, w);
-                mask_edges<64, 1, 1>(k, cc + lane, w);
-                acc = sum_le<1, 1>(w, acc);
-            }
-            const uint32_t sum = group_allreduce<64>(acc);
-            mine = lane == o ? sum : mine;
-        }
-        odd = r0 & 1;
-        const uint64_t b0 = start & ~15ull;
-        const uint32_t s0 = static_cast<uint32_t>(start & 15);
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            // bytes [s0, s0 + len) of the 80 from b0 (keep_bytes works per dword)
-            const uint4 y = own_chunk<BUF>(a, rsrc, recs, b0, (len && ok) ? s0 + len : 0u, i);
-            const int lo = static_cast<int>(s0) - 16 * i, hi = static_cast<int>(s0 + len) - 16 * i;
-            own[i] = make_uint4(keep_bytes(y.x, lo, hi, 0), keep_bytes(y.y, lo, hi, 4), keep_bytes(y.z, lo, hi, 8),
-                                keep_bytes(y.w, lo, hi, 12));
-        }
-    }
-    uint32_t l4_res = 0;
-    const uint8_t stv = rx_finish<5>(a, own, mine, static_cast<uint32_t>(start & 15), len, odd, false,
-                                     live && ok && len != 0, l4_res);
-    if (live) {
-        a.status[p] = stv;
-        if (a.l4_out)
-            a.l4_out[p] = static_cast<uint16_t>(l4_res);
     }
 }
 
@@ -3099,20 +2884,13 @@ int rns_rx_verify_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64
     a.l4_out = d_l4_sum;
     a.local4_sum = be_sum(local_ipv4, 4);
     a.local6_sum = be_sum(local_ipv6, 16);
-    const uint64_t waves = (static_cast<uint64_t>(n) + 63) / 64;  // 64 datagrams per wave
     constexpr int BLK = kMixedBlock<true>;
-    (void)waves;
     const dim3 grid(static_cast<uint32_t>(stash_blocks(n, arena_bytes, true))), block(BLK);
     hipStream_t st = static_cast<hipStream_t>(stream);
-#ifdef RNS_RX_PLAIN
-    constexpr bool kNT = false;
-#else
-    constexpr bool kNT = true;
-#endif
-    if (buf_records(a) < kOobOffset)
-        hipLaunchKernelGGL((csum_mixed_kernel<false, kNT, true, false, true>), grid, block, 0, st, a);
+    if (buf_records(a) < kOobOffset)  // nontemporal loads
+        hipLaunchKernelGGL((csum_mixed_kernel<false, true, true, false, true>), grid, block, 0, st, a);
     else
-        hipLaunchKernelGGL((csum_mixed_kernel<false, kNT, false, false, true>), grid, block, 0, st, a);
+        hipLaunchKernelGGL((csum_mixed_kernel<false, true, false, false, true>), grid, block, 0, st, a);
     return hip_status(hipGetLastError());
 }
 
@@ -3138,18 +2916,6 @@ int rns_rx_verify_packed_dev(const uint8_t *d_arena, uint64_t arena_bytes, const
     a.l4_out = d_l4_sum;
     a.local4_sum = be_sum(local_ipv4, 4);
     a.local6_sum = be_sum(local_ipv6, 16);
-    // ACK-sized datagrams (arena bytes per datagram <= 128): the row-stream form, whose owners
-    // take their datagrams whole (64 B: 13.3 -> 12.1 us per step, session r04b); larger ones
-    // the stream kernel's stash (IMIX verify 478 vs 496 us with rx_rows_kernel).
-    if (RNS_RX_ROWS && a.arena_bytes / n <= 128) {
-        const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(n) + 63) / 64)), block(64);
-        hipStream_t st = static_cast<hipStream_t>(stream);
-        if (buf_records(a) < kOobOffset)
-            hipLaunchKernelGGL((rx_rows_kernel<RNS_STREAM_NT != 0, true>), grid, block, 0, st, a);
-        else
-            hipLaunchKernelGGL((rx_rows_kernel<RNS_STREAM_NT != 0, false>), grid, block, 0, st, a);
-        return hip_status(hipGetLastError());
-    }
     return launch_stream_rx(a, static_cast<hipStream_t>(stream));
 }
 
@@ -3493,8 +3259,8 @@ const char *rns_csum_shape_name(uint32_t len_hint)
 const char *rns_build_info(void)
 {
     return "rns_checksum abi=1 offload-arch=gfx950 kernels=csum_rows_kernel (packed form: 1 KiB rows per 64-packet "
-           "region, owners capture two region prefixes and sum their own end chunk), rx_rows_kernel (its receive-verify "
-           "form for ACK-sized datagrams), csum_stream_kernel (receive verify with an LDS stash), csum_mixed_kernel "
+           "region, owners capture two region prefixes and sum their own end chunk), csum_stream_kernel (receive "
+           "verify: LDS header stash; ACK-sized units owner-loaded), csum_mixed_kernel "
            "(per-wave size-class sort; verify / fill / transmit-finalize stash modes), csum_rounds_kernel, "
            "csum_batch_kernel, csum_chain_kernel (one pass, per-fragment fold) (v_sad_u16 LE sums, v_dot4 BE sums past "
            "128 KiB, wave64, DPP reductions)";

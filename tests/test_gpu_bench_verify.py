@@ -20,8 +20,7 @@ def test_bench_verify_rejects_exactly_the_corrupted(config, steps):
     assert v["rejected_total"] == v["rejected_expected"]
     assert v["datagrams_total"] > 0
     assert line["metric"] == bench.METRIC_VERIFY
-    # ACK-sized datagrams (c2): the row-stream form; larger ones the stash stream kernel
-    assert line["roofline"]["kernel"].startswith("rx_rows_kernel" if config == "c2_64B" else "csum_stream_kernel<RX>")
+    assert line["roofline"]["kernel"].startswith("csum_stream_kernel<RX>")
     assert 0 < line["roofline"]["frac"] < 1.0
     assert line["cpu_baseline"] is None
 
