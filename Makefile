@@ -19,7 +19,12 @@ $(CABI_TEST): tests/c/test_batch_abi.c oracle/csum_oracle.c include/rns_checksum
 	    tests/c/test_batch_abi.c oracle/csum_oracle.c -L$(PKG) -lrns_checksum -Wl,-rpath,'$$ORIGIN/../../$(PKG)' \
 	    -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib -lpthread -o $@
 
-$(BUILD)/rns_checksum.o: $(CSRC)/rns_checksum.hip include/rns_checksum.h
+# One translation unit per kernel family (rns_launch.hpp), compiled in parallel (make -j).
+HIP_SRCS := $(wildcard $(CSRC)/*.hip)
+HIP_HDRS := $(wildcard $(CSRC)/*.hpp) include/rns_checksum.h
+HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(HIP_SRCS))
+
+$(BUILD)/%.o: $(CSRC)/%.hip $(HIP_HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -Iinclude -c $< -o $@
 
@@ -31,32 +36,38 @@ $(BUILD)/host_io.o: $(CSRC)/host_io.cpp include/rns_checksum.h
 	@mkdir -p $(BUILD)
 	g++ $(CXXFLAGS) -Iinclude -c $< -o $@
 
-$(LIB): $(BUILD)/rns_checksum.o $(BUILD)/host_checksum.o $(BUILD)/host_io.o
+$(LIB): $(HIP_OBJS) $(BUILD)/host_checksum.o $(BUILD)/host_io.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
 
 oracle:
 	$(MAKE) -C oracle
 
-# A/B experiment build: `make ab ABDEF="-DRNS_CLASS_U=1,4,4,3,4" ABNAME=u3` -> tools/ab/librns_checksum_u3.so
-# (load it with RNS_CHECKSUM_LIB=...).  Knobs: RNS_CLASS_LOG2G / RNS_CLASS_U (mixed-kernel class shapes),
-# RNS_MIXED_OCC (waves/SIMD bound), RNS_FILL_BLOCK, RNS_FILL_NOSTORE, RNS_RX_PLAIN.
-ABDEF  ?= -DRNS_CLASS_U=1,4,4,3,4
-ABNAME ?= u3
-AB_LIB := tools/ab/librns_checksum_$(ABNAME).so
-$(AB_LIB): $(CSRC)/rns_checksum.hip $(BUILD)/host_checksum.o $(BUILD)/host_io.o include/rns_checksum.h
-	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) $(ABDEF) -Iinclude -c $< -o $(BUILD)/rns_checksum_$(ABNAME).o
+# A/B experiment build: `make -j8 ab ABDEF="-DRNS_ROWS_D=4" ABNAME=d4` -> tools/ab/librns_checksum_d4.so
+# (load it with RNS_CHECKSUM_LIB=...).  Knobs: RNS_CLASS_LOG2G / RNS_CLASS_U (class-kernel shapes),
+# RNS_MIXED_OCC / RNS_FILL_OCC / RNS_CHAIN_OCC (waves/SIMD bounds), RNS_ROWS_D, RNS_STREAM_MAXLEN, ...
+ABDEF  ?= -DRNS_ROWS_D=4
+ABNAME ?= d4
+AB_BUILD := $(BUILD)/ab_$(ABNAME)
+AB_OBJS  := $(patsubst $(CSRC)/%.hip,$(AB_BUILD)/%.o,$(HIP_SRCS))
+AB_LIB   := tools/ab/librns_checksum_$(ABNAME).so
+$(AB_BUILD)/%.o: $(CSRC)/%.hip $(HIP_HDRS)
+	@mkdir -p $(AB_BUILD)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) $(ABDEF) -Iinclude -c $< -o $@
+$(AB_LIB): $(AB_OBJS) $(BUILD)/host_checksum.o $(BUILD)/host_io.o
 	@mkdir -p tools/ab
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(BUILD)/rns_checksum_$(ABNAME).o $(BUILD)/host_checksum.o $(BUILD)/host_io.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
 
 ab: $(AB_LIB)
 
 # Register / occupancy report for every kernel instantiation.
-resources: $(CSRC)/rns_checksum.hip
-	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -Iinclude -c $< -o /dev/null -Rpass-analysis=kernel-resource-usage
+resources: $(HIP_OBJS)
+	for o in $(HIP_OBJS); do bash tools/scratch_report.sh $$o | tail -n +2; done | sort -k3 | \
+	    awk 'BEGIN { print "scratch_B_per_lane\tvgprs\tkernel" } { print }'
 
-asm: $(CSRC)/rns_checksum.hip
+asm: $(HIP_SRCS)
 	@mkdir -p $(BUILD)/asm
-	cd $(BUILD)/asm && $(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -I../../../include -c ../../../$< -o rns.o -save-temps
+	for f in $(HIP_SRCS); do (cd $(BUILD)/asm && $(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -I../../../include \
+	    --cuda-device-only -S ../../../$$f -o $$(basename $$f .hip).s) || exit 1; done
 
 clean:
 	rm -rf $(BUILD) $(LIB) $(CABI_TEST)

@@ -21,9 +21,9 @@ rank's u16 results (as uint8, 2 B per packet) per step, and `gather_ms` = the
 all-gather alone.  Rank 0 prints one JSON line.
 
 Descriptors (--desc auto): the packed form (rns_csum_batch_packed_dev: u16 length and
-u16 seed per packet, one u64 offset per 64 packets) — the synthetic batches are packed
-at 16-byte alignment — except for jumbo batches, whose group kernel has no 64-packet
-wave batches: they take the compact form (u32 offsets).
+u16 seed per packet, one u64 offset per 64 packets; the synthetic batches are packed at
+16-byte alignment, and the rows kernel streams them), except the tiny fixed-size c2
+batch, which takes the strided form (seeds only; no offsets or lengths at all).
 
 Kernel time: one event pair around the K back-to-back timed launches gives the
 per-launch mean (`kernel_avg_us`) from which `roofline.frac` is computed.  A
@@ -67,8 +67,8 @@ def parse_args(argv=None):
                         "(rns_csum_batch_dev_off32); packed = u16 lengths + one offset per 64 packets "
                         "(rns_csum_batch_packed_dev); strided = equal-length packets at a fixed stride, no "
                         "offset or length descriptors (rns_csum_batch_strided_dev; fixed-size configs only); "
-                        "auto = strided for tiny equal-length packets (c2), packed otherwise, except for jumbo batches (the group "
-                        "kernel, which has no 64-packet wave batches): 32 below 4 GiB, else 64")
+                        "auto = strided for tiny equal-length packets (c2), packed otherwise (u16 lengths: packets "
+                        "above 65535 B take 32 below 4 GiB, else 64)")
     p.add_argument("--shape", default="", help="variant,G,U,max_blocks kernel shape override (tuning)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample duration (single thread)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -355,11 +355,12 @@ class GpuEngine:
         form = {True: "32", False: "64"}.get(compact, compact)
         if form == "auto":
             small = self.layout.arena_bytes + 16 < 2 ** 32
-            jumbo = self.layout.mean_len > 2500  # pick_shape's group kernel: no wave batches, no packed form
+            # the packed form takes u16 lengths (an IP datagram's length field)
+            packable = self.layout.n == 0 or int(self.layout.length.max()) <= 0xFFFF
             # tiny equal-length packets at a fixed stride (c2): the strided form, whose offsets need no
             # descriptor load before a wave's first data load (isolated 13.68 -> 12.98 us, r03h)
             tiny_fixed = op == "csum" and self.layout.mean_len < 128 and self.batches[0].stride() is not None
-            form = "64" if shape is not None else ("strided" if tiny_fixed else "packed" if not jumbo else
+            form = "64" if shape is not None else ("strided" if tiny_fixed else "packed" if packable else
                                                    ("32" if small else "64"))
         if op == "verify":  # packed receive arena (16-byte-aligned datagrams): the stream kernel; else 64-bit
             from rustnetworkstack_amd.workloads import make_verify_batch
@@ -512,7 +513,7 @@ class GpuEngine:
                         "ACK-sized datagrams: owners load their datagrams whole)")
             return "csum_mixed_kernel<RX> (rns_rx_verify_dev: class-sorted data pass + header stash)"
         mean = self.layout.mean_len
-        if self.packed and self.layout.n and int(self.layout.off[0]) % 16 == 0 and 112 < mean <= 1200:
+        if self.packed and self.layout.n and int(self.layout.off[0]) % 16 == 0 and mean > 112:
             return ("csum_rows_kernel (packed form, 16-byte-aligned packets: one wave streams each 64-packet "
                     "block as 1 KiB rows; owners capture two region prefixes and sum their own end chunk)")
         return _lib.load().rns_csum_shape_name(int(round(self.layout.mean_len))).decode()

@@ -1,0 +1,74 @@
+// The packed form (rns_csum_batch_packed_dev) and packed receive verify.
+#include "rns_launch.hpp"
+
+namespace rns {
+
+// The packed form's kernels (separate instantiations, so the explicit-descriptor
+// kernels carry no packed-form code): the mixed kernel, or for tiny packets the
+// rounds kernel with pick_shape's G=4, U=1 shape.
+// Receive verify's stream launch: one wave per 64-datagram unit.
+int launch_stream_rx(const CsumArgs &a, hipStream_t st)
+{
+    const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);
+    if (buf_records(a) < kOobOffset)
+        hipLaunchKernelGGL((csum_stream_kernel<RNS_STREAM_NT != 0, true>), grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL((csum_stream_kernel<RNS_STREAM_NT != 0, false>), grid, block, 0, st, a);
+    return hip_status(hipGetLastError());
+}
+
+int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
+{
+    const bool nt = (sh.variant & 2u) != 0, buf = buf_records(a) < kOobOffset;
+    // 16-byte-aligned packets (align_log2 >= 4) of any typical length above the tiny rounds
+    // kernel's, or unknown: the rows kernel.  Measured against the kernels it replaced (session
+    // r04d, isolated dispatch): c3 1500 B 231.5 vs 238.5-239.2 us (class kernel), c4 9000 B
+    // 344.4-345.1 vs 346.4-347.1 (group kernel, u32 offsets), IMIX 451-453 vs 456 (round 3's
+    // stream kernel).  Tiny packets keep the rounds kernel (c2: 13.2-13.7 vs 14.0-14.8 us with
+    // round 3's stream kernel).
+    const bool tiny = (sh.variant & ~16u) == 3u && sh.G == 4u && sh.U == 1u;
+    if (a.align_mask >= 15u && !tiny) {
+        const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);
+        if (buf)
+            hipLaunchKernelGGL((csum_rows_kernel<RNS_STREAM_NT != 0, true>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_rows_kernel<RNS_STREAM_NT != 0, false>), grid, block, 0, st, a);
+        return hip_status(hipGetLastError());
+    }
+    const uint64_t batches = (static_cast<uint64_t>(a.n) + 63) / 64;  // one wave per 64 packets
+    const uint64_t wpb = ((sh.variant & 4u) ? kMixedBlock<false> : kBlock) / 64;  // waves per workgroup
+    uint64_t blocks = (batches + wpb - 1) / wpb;
+    if (sh.max_blocks != 0 && blocks > sh.max_blocks)
+        blocks = sh.max_blocks;
+    const dim3 grid(static_cast<uint32_t>(blocks)), block((sh.variant & 4u) ? kMixedBlock<false> : kBlock);
+    if (sh.variant & 4u) {
+        if (nt && buf)
+            hipLaunchKernelGGL((csum_mixed_kernel<false, true, true, false, false, false, true>), grid, block, 0, st, a);
+        else if (nt)
+            hipLaunchKernelGGL((csum_mixed_kernel<false, true, false, false, false, false, true>), grid, block, 0, st, a);
+        else if (buf)
+            hipLaunchKernelGGL((csum_mixed_kernel<false, false, true, false, false, false, true>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_mixed_kernel<false, false, false, false, false, false, true>), grid, block, 0, st,
+                               a);
+    } else if ((sh.variant & ~16u) == 3u && sh.G == 4u && sh.U == 1u) {  // c2: 13.46 -> 13.36 us with prefetch
+        const bool pf = (sh.variant & 16u) != 0;
+#ifndef RNS_PACKED_TINY_D  // A/B knob: 4 = every round of a wave batch issued at once (with the prefetch)
+#define RNS_PACKED_TINY_D 1
+#endif
+        if (buf && pf)
+            hipLaunchKernelGGL((csum_rounds_kernel<4, 1, false, true, true, RNS_PACKED_TINY_D, true, true>), grid, block, 0,
+                               st, a);
+        else if (buf)
+            hipLaunchKernelGGL((csum_rounds_kernel<4, 1, false, true, true, 1, true>), grid, block, 0, st, a);
+        else if (pf)
+            hipLaunchKernelGGL((csum_rounds_kernel<4, 1, false, true, false, 1, true, true>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_rounds_kernel<4, 1, false, true, false, 1, true>), grid, block, 0, st, a);
+    } else {
+        return RNS_E_INVALID;
+    }
+    return hip_status(hipGetLastError());
+}
+
+}  // namespace rns

@@ -21,6 +21,7 @@ implies (and, if present, the event-pair launches' durations).
 import argparse
 import csv
 import json
+import re
 import statistics
 
 
@@ -39,7 +40,11 @@ def main():
     b = json.loads(line)
     W, K = b.get("launches_before_timed", b["warmup"]), b["steps"]
     M = b["roofline"].get("evpair_launches", 0)
-    rows = [r for r in csv.DictReader(open(args.trace)) if args.kernel in r["Kernel_Name"]]
+    # the product kernel is the one the line names (e.g. verify mode's batch is built by the
+    # transmit-finalize kernel first, which also matches "csum_"): its template name + "<"
+    m = re.match(r"[A-Za-z_0-9]+", str(b["roofline"].get("kernel", "")))
+    want = (m.group(0) + "<") if m else args.kernel
+    rows = [r for r in csv.DictReader(open(args.trace)) if args.kernel in r["Kernel_Name"] and want in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     if not rows:
         raise SystemExit("no dispatch of the product kernel in the trace")
