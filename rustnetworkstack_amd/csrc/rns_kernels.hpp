@@ -1945,7 +1945,7 @@ __device__ __forceinline__ uint4 own_chunk(const CsumArgs &a, __amdgpu_buffer_rs
 template <bool NT, bool BUF>
 __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(const CsumArgs a)
 {
-    constexpr int kNS = 5;  // stash chunks per datagram (the unaligned path fills 5)
+    constexpr int kNS = 4;  // stash chunks per datagram (16-byte-aligned: its first 64 bytes)
     // entry bits: [31:17] row tag, [16] head chunk, [15:14] head index, [13] end chunk,
     // [12] first chunk, [11:4] packet (of the wave's 64), [3:0] valid bytes - 1 (end chunk)
     constexpr uint32_t kTagShift = 17, kHead = 1u << 16, kEnd = 1u << 13, kStart = 1u << 12;
@@ -1983,10 +1983,13 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
         // ---- ACK-sized unit: every owner takes its datagram whole ----
         const uint64_t start = r0 + excl;
         const bool ok = start <= a.arena_bytes && len <= a.arena_bytes - start;
-        uint4 own[5];
+        uint4 own[kNS + 1];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)  // all four loads in flight before the first is used
+            own[i] = own_chunk<BUF>(a, rsrc, recs, start, len, i);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            uint4 x = own_chunk<BUF>(a, rsrc, recs, start, len, i);
+            uint4 x = own[i];
             if (16u * i + 16u > len)  // rx_finish sees zeros past the end, as from the stash
                 x = 16u * i < len ? keep_first(x, len - 16u * i) : make_uint4(0, 0, 0, 0);
             own[i] = x;
@@ -1997,7 +2000,7 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
         }
         own[4] = make_uint4(0, 0, 0, 0);
         uint32_t l4_res = 0;
-        const uint8_t stv = rx_finish<kNS>(a, own, mine, 0u, len, false, false, live && ok && len != 0, l4_res);
+        const uint8_t stv = rx_finish<kNS + 1>(a, own, mine, 0u, len, false, false, live && ok && len != 0, l4_res);
         if (live) {
             a.status[p] = stv;
             if (a.l4_out)
@@ -2103,14 +2106,34 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
                 uint4 w[1];
                 issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, w);
                 mask_edges<64, 1, 1>(k, cc + lane, w);
-                if (cc == 0 && lane < static_cast<uint32_t>(kNS))
-                    stash[o * kNS + lane] = lane < k.nch ? w[0] : make_uint4(0, 0, 0, 0);
                 acc = sum_le<1, 1>(w, acc);
             }
             const uint32_t sum = group_allreduce<64>(acc);
             mine = lane == o ? sum : mine;
         }
         odd = r0 & 1;  // every packet of the range shares the region start's misalignment
+        // each owner takes its header from the 16-byte boundary below its start: 5 chunks hold
+        // its first 65-80 bytes, masked to the datagram
+        const uint64_t b0 = start & ~15ull;
+        const uint32_t s0 = static_cast<uint32_t>(start & 15);
+        uint4 own[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+            own[i] = own_chunk<BUF>(a, rsrc, recs, b0, (len && ok) ? s0 + len : 0u, i);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const int lo = static_cast<int>(s0) - 16 * i, hi = static_cast<int>(s0 + len) - 16 * i;
+            own[i] = make_uint4(keep_bytes(own[i].x, lo, hi, 0), keep_bytes(own[i].y, lo, hi, 4),
+                                keep_bytes(own[i].z, lo, hi, 8), keep_bytes(own[i].w, lo, hi, 12));
+        }
+        uint32_t l4_res = 0;
+        const uint8_t stv = rx_finish<5>(a, own, mine, s0, len, odd, false, live && ok && len != 0, l4_res);
+        if (live) {
+            a.status[p] = stv;
+            if (a.l4_out)
+                a.l4_out[p] = static_cast<uint16_t>(l4_res);
+        }
+        return;
     }
     wave_lds_fence();
     const uint64_t start = r0 + excl;
@@ -2151,6 +2174,10 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
 #define RNS_ROWS_D 8  // (c5 isolated 456 -> 451-453 us against 4, session r04c)
 #endif
 constexpr int kRowsD = RNS_ROWS_D;
+#ifndef RNS_ROWS_END_PULL  // A/B knob: 1 = owners pull their end chunk from its row (ds_bpermute), no own load
+#define RNS_ROWS_END_PULL 0
+#endif
+constexpr bool kRowsEndPull = RNS_ROWS_END_PULL != 0;
 template <bool NT, bool BUF>
 __global__ __launch_bounds__(64, RNS_ROWS_OCC) void csum_rows_kernel(const CsumArgs a)
 {
@@ -2183,9 +2210,10 @@ __global__ __launch_bounds__(64, RNS_ROWS_OCC) void csum_rows_kernel(const CsumA
         const uint32_t nrows = (total + 1023) >> 10;
         const uint32_t c0 = excl >> 4;
         const uint32_t e = len ? (excl + len - 1) >> 4 : c0;
-        // the end chunk, first: its line is then an L2 hit for the row that streams it
-        uint4 endv;
-        {
+        // the end chunk, first: its line is then an L2 hit for the row that streams it (or, with
+        // RNS_ROWS_END_PULL, pulled from the lane that loads it in its row: no extra load)
+        uint4 endv = make_uint4(0, 0, 0, 0);
+        if constexpr (!kRowsEndPull) {
             const uint64_t off = r0 + (static_cast<uint64_t>(e) << 4);
             const bool in = len != 0 && off + 16 <= recs;
             if constexpr (BUF) {
@@ -2219,14 +2247,20 @@ __global__ __launch_bounds__(64, RNS_ROWS_OCC) void csum_rows_kernel(const CsumA
             __builtin_amdgcn_sched_barrier(0);
         }
         // the owner's partial end chunk (its padding bytes never count)
-        uint32_t part = 0;
-        if (len) {
-            const uint4 x = keep_first(endv, ((len - 1) & 15u) + 1u);
-            part = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
-            part = __builtin_amdgcn_sad_u16(x.y, 0, part);
-            part = __builtin_amdgcn_sad_u16(x.z, 0, part);
-            part = __builtin_amdgcn_sad_u16(x.w, 0, part);
-        }
+        auto partial = [&]() {
+            uint32_t pt = 0;
+            if (len) {
+                const uint4 x = keep_first(endv, ((len - 1) & 15u) + 1u);
+                pt = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
+                pt = __builtin_amdgcn_sad_u16(x.y, 0, pt);
+                pt = __builtin_amdgcn_sad_u16(x.z, 0, pt);
+                pt = __builtin_amdgcn_sad_u16(x.w, 0, pt);
+            }
+            return pt;
+        };
+        uint32_t part = kRowsEndPull ? 0u : partial();
+        const uint32_t row_e = len ? e >> 6 : 0xFFFFFFFFu;
+        const int src_e = static_cast<int>((e & 63u) << 2);
         // capture points: P(c0 - 1) and P(e - 1) (row, source lane); e == c0 takes the
         // start's point twice (the difference is 0), c0 == 0 never captures (P(-1) = 0)
         const uint32_t ca = c0 - 1u;
@@ -2243,6 +2277,16 @@ __global__ __launch_bounds__(64, RNS_ROWS_OCC) void csum_rows_kernel(const CsumA
                 s = __builtin_amdgcn_sad_u16(x.y, 0, s);
                 s = __builtin_amdgcn_sad_u16(x.z, 0, s);
                 s = __builtin_amdgcn_sad_u16(x.w, 0, s);
+                if constexpr (kRowsEndPull) {
+                    if (__ballot(row_e == k)) {  // owners whose end chunk is in this row pull it
+                        const uint4 y = make_uint4(
+                            static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_e, static_cast<int>(x.x))),
+                            static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_e, static_cast<int>(x.y))),
+                            static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_e, static_cast<int>(x.z))),
+                            static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_e, static_cast<int>(x.w))));
+                        endv = row_e == k ? y : endv;
+                    }
+                }
                 // the row D ahead into the registers this row just freed (issued after the row
                 // is consumed: no loop-carried copy, exact vmcnt(D-1) waits)
                 __builtin_amdgcn_sched_barrier(0);
@@ -2256,6 +2300,8 @@ __global__ __launch_bounds__(64, RNS_ROWS_OCC) void csum_rows_kernel(const CsumA
                 carry += __builtin_amdgcn_readlane(inc, 63);
             }
         }
+        if constexpr (kRowsEndPull)
+            part = partial();
         mine = len ? pb - pa + part : 0u;
     } else {
         // ---- unaligned region (rare): the whole wave sums one packet at a time ----
