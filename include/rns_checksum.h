@@ -125,7 +125,9 @@ int rns_csum_batch_dev_off32(const uint8_t *d_arena, uint64_t arena_bytes, const
  * 16 bits) plus d_blk_off[b] = the offset of packet 64*b, one u64 per 64 packets
  * (rns_packed_layout computes them): 2.1 B of descriptors per packet instead of
  * 10 (off32) or 14.  Per packet exactly util.rs:88-110, as rns_csum_batch_dev;
- * a packet outside the arena gets 0 and is counted in *d_bad. */
+ * a packet outside the arena gets 0 and is counted in *d_bad.  With align_log2 >= 4
+ * every batch but one of tiny packets (len_hint <= 112) is streamed as whole 1 KiB
+ * rows of its 64-packet blocks, whatever the packet sizes (the rows kernel). */
 int rns_csum_batch_packed_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_blk_off,
                               const uint16_t *d_len16, uint32_t align_log2, const uint16_t *d_seed, uint16_t *d_out,
                               uint32_t n, uint32_t flags, uint32_t len_hint, uint32_t *d_bad, void *stream);
@@ -208,9 +210,9 @@ int rns_rx_verify_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64
  * with datagrams starting on 16-byte boundaries (align_log2 >= 4; 2048-byte receive
  * slots qualify): per datagram exactly the checks and status bits of rns_rx_verify_dev
  * (ip.rs:65-131, tcp.rs:838-850, icmp.rs:44-75).  One wave streams each 64-datagram
- * block's bytes as whole 1 KiB rows whatever the datagram sizes (the stream kernel),
- * which keeps ACK-sized datagrams at the plain checksum's rate.  align_log2 < 4 is
- * RNS_E_INVALID. */
+ * block's bytes as whole 1 KiB rows whatever the datagram sizes (the stream kernel);
+ * a block of ACK-sized datagrams (all <= 64 B) is read by its owners directly, which
+ * keeps them at the plain checksum's rate.  align_log2 < 4 is RNS_E_INVALID. */
 int rns_rx_verify_packed_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_blk_off,
                              const uint16_t *d_len16, uint32_t align_log2, uint32_t n, const uint8_t *local_ipv4,
                              const uint8_t *local_ipv6, uint8_t *d_status, uint16_t *d_l4_sum, void *stream);
