@@ -28,14 +28,22 @@ int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
     // round 3's stream kernel).
     const bool tiny = (sh.variant & ~16u) == 3u && sh.G == 4u && sh.U == 1u;
     if (a.align_mask >= 15u && !tiny) {
-        const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);
-#ifndef RNS_ROWS_LDS  // A/B knob: LDS bytes reserved per one-wave workgroup (caps waves per CU; 0 = none)
-#define RNS_ROWS_LDS 0
+#ifndef RNS_ROWS_DEEP_FROM  // typical lengths from this take D = 16 rows in flight at 4 waves/SIMD
+#define RNS_ROWS_DEEP_FROM 1024u
 #endif
-        if (buf)
-            hipLaunchKernelGGL((csum_rows_kernel<RNS_STREAM_NT != 0, true>), grid, block, RNS_ROWS_LDS, st, a);
-        else
-            hipLaunchKernelGGL((csum_rows_kernel<RNS_STREAM_NT != 0, false>), grid, block, RNS_ROWS_LDS, st, a);
+        constexpr bool NT = RNS_STREAM_NT != 0;
+        const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);
+        if (a.len_hint >= RNS_ROWS_DEEP_FROM) {
+            if (buf)
+                hipLaunchKernelGGL((csum_rows_kernel<NT, true, 16>), grid, block, 0, st, a);
+            else
+                hipLaunchKernelGGL((csum_rows_kernel<NT, false, 16>), grid, block, 0, st, a);
+        } else {
+            if (buf)
+                hipLaunchKernelGGL((csum_rows_kernel<NT, true, 8>), grid, block, 0, st, a);
+            else
+                hipLaunchKernelGGL((csum_rows_kernel<NT, false, 8>), grid, block, 0, st, a);
+        }
         return hip_status(hipGetLastError());
     }
     const uint64_t batches = (static_cast<uint64_t>(a.n) + 63) / 64;  // one wave per 64 packets

@@ -2167,19 +2167,12 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
 // (csum_stream_kernel: a table publish, two wave fences, the masks; 57 VALU/KB).
 // u32 differences are exact: a packet's LE word sum is < 2^32.
 // ---------------------------------------------------------------------------
-#ifndef RNS_ROWS_OCC
-#define RNS_ROWS_OCC 8
-#endif
-#ifndef RNS_ROWS_D  // rows (1 KiB loads) in flight per wave
-#define RNS_ROWS_D 8  // (c5 isolated 456 -> 451-453 us against 4, session r04c)
-#endif
-constexpr int kRowsD = RNS_ROWS_D;
-#ifndef RNS_ROWS_END_PULL  // A/B knob: 1 = owners pull their end chunk from its row (ds_bpermute), no own load
-#define RNS_ROWS_END_PULL 0
-#endif
-constexpr bool kRowsEndPull = RNS_ROWS_END_PULL != 0;
-template <bool NT, bool BUF>
-__global__ __launch_bounds__(64, RNS_ROWS_OCC) void csum_rows_kernel(const CsumArgs a)
+// Rows in flight D: 8 at 8 waves/SIMD, or 16 at 4 waves/SIMD for MTU-sized and longer packets
+// (c3 isolated 230.2-231.0 -> 227.8-227.9 us; IMIX 445.6-447.6 -> 454-456, so IMIX keeps 8;
+// D = 12 at 5 waves/SIMD in between; two or four 64-packet sets per wave slower on IMIX:
+// session r04g).
+template <bool NT, bool BUF, int D>
+__global__ __launch_bounds__(64, D >= 16 ? 4 : 8) void csum_rows_kernel(const CsumArgs a)
 {
     const uint32_t lane = threadIdx.x;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -2210,10 +2203,11 @@ __global__ __launch_bounds__(64, RNS_ROWS_OCC) void csum_rows_kernel(const CsumA
         const uint32_t nrows = (total + 1023) >> 10;
         const uint32_t c0 = excl >> 4;
         const uint32_t e = len ? (excl + len - 1) >> 4 : c0;
-        // the end chunk, first: its line is then an L2 hit for the row that streams it (or, with
-        // RNS_ROWS_END_PULL, pulled from the lane that loads it in its row: no extra load)
-        uint4 endv = make_uint4(0, 0, 0, 0);
-        if constexpr (!kRowsEndPull) {
+        // the end chunk, first: its line is then an L2 hit for the row that streams it, if it is
+        // still there (pulling it from its row instead, four ds_bpermute per row, measured 2x
+        // slower: session r04g)
+        uint4 endv;
+        {
             const uint64_t off = r0 + (static_cast<uint64_t>(e) << 4);
             const bool in = len != 0 && off + 16 <= recs;
             if constexpr (BUF) {
@@ -2227,7 +2221,7 @@ __global__ __launch_bounds__(64, RNS_ROWS_OCC) void csum_rows_kernel(const CsumA
         }
         __builtin_amdgcn_sched_barrier(0);
         const uint32_t vlane = lane << 4;
-        uint4 v[kRowsD];
+        uint4 v[D];
         auto issue = [&](uint32_t k, uint4 &dst) {  // row k: chunk 64k + lane of the region
             if constexpr (BUF) {
                 // wave-uniform row base (a row past the region: out of range, no traffic)
@@ -2242,25 +2236,19 @@ __global__ __launch_bounds__(64, RNS_ROWS_OCC) void csum_rows_kernel(const CsumA
             }
         };
 #pragma unroll
-        for (int j = 0; j < kRowsD; ++j) {
+        for (int j = 0; j < D; ++j) {
             issue(j, v[j]);
             __builtin_amdgcn_sched_barrier(0);
         }
         // the owner's partial end chunk (its padding bytes never count)
-        auto partial = [&]() {
-            uint32_t pt = 0;
-            if (len) {
-                const uint4 x = keep_first(endv, ((len - 1) & 15u) + 1u);
-                pt = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
-                pt = __builtin_amdgcn_sad_u16(x.y, 0, pt);
-                pt = __builtin_amdgcn_sad_u16(x.z, 0, pt);
-                pt = __builtin_amdgcn_sad_u16(x.w, 0, pt);
-            }
-            return pt;
-        };
-        uint32_t part = kRowsEndPull ? 0u : partial();
-        const uint32_t row_e = len ? e >> 6 : 0xFFFFFFFFu;
-        const int src_e = static_cast<int>((e & 63u) << 2);
+        uint32_t part = 0;
+        if (len) {
+            const uint4 x = keep_first(endv, ((len - 1) & 15u) + 1u);
+            part = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
+            part = __builtin_amdgcn_sad_u16(x.y, 0, part);
+            part = __builtin_amdgcn_sad_u16(x.z, 0, part);
+            part = __builtin_amdgcn_sad_u16(x.w, 0, part);
+        }
         // capture points: P(c0 - 1) and P(e - 1) (row, source lane); e == c0 takes the
         // start's point twice (the difference is 0), c0 == 0 never captures (P(-1) = 0)
         const uint32_t ca = c0 - 1u;
@@ -2268,29 +2256,19 @@ __global__ __launch_bounds__(64, RNS_ROWS_OCC) void csum_rows_kernel(const CsumA
         const uint32_t row_a = c0 ? ca >> 6 : 0xFFFFFFFFu, row_b = (e > c0 || c0) ? cb >> 6 : 0xFFFFFFFFu;
         const int src_a = static_cast<int>((ca & 63u) << 2), src_b = static_cast<int>((cb & 63u) << 2);
         uint32_t pa = 0, pb = 0, carry = 0;
-        for (uint32_t k0 = 0; k0 < nrows; k0 += kRowsD) {
+        for (uint32_t k0 = 0; k0 < nrows; k0 += D) {
 #pragma unroll
-            for (int j = 0; j < kRowsD; ++j) {
+            for (int j = 0; j < D; ++j) {
                 const uint32_t k = k0 + j;
                 const uint4 x = v[j];
                 uint32_t s = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
                 s = __builtin_amdgcn_sad_u16(x.y, 0, s);
                 s = __builtin_amdgcn_sad_u16(x.z, 0, s);
                 s = __builtin_amdgcn_sad_u16(x.w, 0, s);
-                if constexpr (kRowsEndPull) {
-                    if (__ballot(row_e == k)) {  // owners whose end chunk is in this row pull it
-                        const uint4 y = make_uint4(
-                            static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_e, static_cast<int>(x.x))),
-                            static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_e, static_cast<int>(x.y))),
-                            static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_e, static_cast<int>(x.z))),
-                            static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_e, static_cast<int>(x.w))));
-                        endv = row_e == k ? y : endv;
-                    }
-                }
                 // the row D ahead into the registers this row just freed (issued after the row
                 // is consumed: no loop-carried copy, exact vmcnt(D-1) waits)
                 __builtin_amdgcn_sched_barrier(0);
-                issue(k + kRowsD, v[j]);
+                issue(k + D, v[j]);
                 __builtin_amdgcn_sched_barrier(0);
                 const uint32_t inc = wave_incl_scan(s);
                 const uint32_t ta = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_a, static_cast<int>(inc)));
@@ -2300,8 +2278,6 @@ __global__ __launch_bounds__(64, RNS_ROWS_OCC) void csum_rows_kernel(const CsumA
                 carry += __builtin_amdgcn_readlane(inc, 63);
             }
         }
-        if constexpr (kRowsEndPull)
-            part = partial();
         mine = len ? pb - pa + part : 0u;
     } else {
         // ---- unaligned region (rare): the whole wave sums one packet at a time ----
