@@ -122,11 +122,17 @@ def parse_args(argv=None):
     return args
 
 
-def auto_graph_streams(mean_len: float) -> int:
+def auto_graph_streams(mean_len: float, step_bytes: float = 0.0) -> int:
     """Streams the graph-mode timed steps alternate over (profiles/archive/r02/r02_graph_streams.json, and
-    r03 with every concurrently running step reading its own batch): 3 for tiny packets, 4 for
-    small mixed ones, 2 for MTU and jumbo batches."""
-    return 3 if mean_len < 128 else 4 if mean_len < 1000 else 2
+    r03/r04 with every concurrently running step reading its own batch): 3 for tiny packets, 2 for
+    MTU and jumbo batches and for small mixed ones, 1 for a small-mixed step of a GiB or more
+    (session r04h, rows kernel: 2^23 IMIX 452.5 / 462.0 / 468.6 / 469.7 us per step at 1 / 2 / 3 / 4
+    streams, its 2^20 shard 58.8 / 58.3 / - / 60.4; c3 229.6 / 224.4 / 228.0)."""
+    if mean_len < 128:
+        return 3
+    if mean_len < 1000 and step_bytes >= (1 << 30):
+        return 1
+    return 2
 
 
 # ---------------------------------------------------------------------------
@@ -757,7 +763,12 @@ def main(argv=None):
         strong = True
     if args.graph_streams <= 0:
         from rustnetworkstack_amd.workloads import make_layout
-        args.graph_streams = auto_graph_streams(make_layout(args.config, n=4096).mean_len)
+        from rustnetworkstack_amd.workloads import CONFIGS
+        mean = make_layout(args.config, n=4096).mean_len
+        per_rank = CONFIGS[args.config]["n"] if args.config in CONFIGS else 0
+        if strong:  # the rank's shard of the config's one batch
+            per_rank = -(-per_rank // (args.shard_rw[1] if args.shard_rw is not None else dist.world))
+        args.graph_streams = auto_graph_streams(mean, per_rank * mean)
     # min_batches is a hint for the graph path (one batch per graph stream); an engine
     # that is not on a GPU ignores it, and the graph decision follows the engine's device
     engine = GpuEngine(args.config, dist.rank, dist.local_rank, shape=shape, steps=args.steps, world=dist.world,
