@@ -184,6 +184,21 @@ int rns_csum_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_
                       const uint16_t *d_seed, const uint16_t *d_field, uint32_t field_off, uint16_t *d_out,
                       uint32_t n, uint32_t flags, uint32_t *d_bad, void *stream);
 
+/* Transmit in-place fill of a PACKED transmit arena (the descriptor form of
+ * rns_csum_batch_packed_dev: u16 lengths, d_blk_off[b] = offset of packet 64*b,
+ * packets back to back at 2^align_log2 boundaries, align_log2 >= 4): per packet exactly
+ * what rns_csum_fill_dev does (tcp.rs:957-973, udp.rs:158-171, icmp.rs:87-112,
+ * ip.rs:158-159) — the field at d_field[i] (NULL => field_off) counted as zero, the
+ * result stored big-endian into it, d_out (optional) and *d_bad as there.  One wave
+ * streams each 64-packet block's bytes as whole 1 KiB rows (the rows kernel); the owner
+ * of a packet rewrites the 32-byte sector around its field when it lies inside the
+ * packet.  len_hint = the typical packet length (kernel depth).  align_log2 < 4 is
+ * RNS_E_INVALID. */
+int rns_csum_fill_packed_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_blk_off, const uint16_t *d_len16,
+                             uint32_t align_log2, const uint16_t *d_seed, const uint16_t *d_field, uint32_t field_off,
+                             uint16_t *d_out, uint32_t n, uint32_t flags, uint32_t len_hint, uint32_t *d_bad,
+                             void *stream);
+
 /* Receive verify (§8f row 1): for each received IP datagram
  * d_arena[d_off[i] .. + d_len[i]), the checks the stack applies before handing it
  * to the transport layer — ip_input_v4 header checksum (ip.rs:76-80), fragment

@@ -386,6 +386,49 @@ def csum_fill(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, seed
     return out
 
 
+def csum_fill_packed(arena: torch.Tensor, blk_off: torch.Tensor, len16: torch.Tensor,
+                     seed: torch.Tensor | None = None, *, align_log2: int = 4, field: torch.Tensor | None = None,
+                     field_off: int = 16, complement: bool = True, out: torch.Tensor | None = None,
+                     len_hint: int = 0, bad: torch.Tensor | None = None) -> torch.Tensor | None:
+    """Transmit in-place fill of a packed arena (rns_csum_fill_packed_dev): ``csum_fill``'s
+    result and stores, with the packed form's descriptors (see PackedBatch; align_log2 >= 4)."""
+    _require_cuda(arena, "arena", (torch.uint8,))
+    _require_cuda(blk_off, "blk_off", (torch.int64,))
+    _require_cuda(len16, "len16", _U16)
+    n = len16.numel()
+    if blk_off.numel() != (n + 63) // 64:
+        raise ValueError("blk_off must have one entry per 64 packets")
+    if not 4 <= align_log2 <= 12:
+        raise ValueError("the packed fill needs align_log2 in 4..12")
+    dev = arena.device
+    ptrs = []
+    for name, t in (("blk_off", blk_off), ("len16", len16)):
+        if t.device != dev:
+            raise ValueError(f"{name} is on {t.device}, arena on {dev}")
+    for name, t in (("seed", seed), ("field", field), ("out", out)):
+        if t is None:
+            ptrs.append(None)
+            continue
+        _require_cuda(t, name, _U16)
+        if t.numel() != n or t.device != dev:
+            raise ValueError(f"{name} must have one entry per packet on the arena's device")
+        ptrs.append(t.data_ptr())
+    bad_ptr = None
+    if bad is not None:
+        _require_cuda(bad, "bad", (torch.int32,))
+        if bad.device != dev:
+            raise ValueError(f"bad is on {bad.device}, arena on {dev}")
+        bad_ptr = bad.data_ptr()
+    lib = _lib.load()
+    with torch.cuda.device(dev):
+        st = lib.rns_csum_fill_packed_dev(arena.data_ptr(), arena.numel(), blk_off.data_ptr(), len16.data_ptr(),
+                                          int(align_log2), ptrs[0], ptrs[1], int(field_off), ptrs[2], n,
+                                          _lib.RNS_FLAG_COMPLEMENT if complement else 0, int(len_hint), bad_ptr,
+                                          _stream_handle(dev))
+    _lib.check(st, "rns_csum_fill_packed_dev")
+    return out
+
+
 def rx_verify(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, local_ipv4: bytes, local_ipv6: bytes,
               *, status: torch.Tensor | None = None, l4_sum: torch.Tensor | None = None) -> torch.Tensor:
     """Receive verify of a batch of IP datagrams (rns_rx_verify_dev): returns a uint8

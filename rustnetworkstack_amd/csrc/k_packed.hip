@@ -1,6 +1,10 @@
 // The packed form (rns_csum_batch_packed_dev) and packed receive verify.
 #include "rns_launch.hpp"
 
+#ifndef RNS_ROWS_DEEP_FROM  // typical lengths from this take D = 16 rows in flight at 4 waves/SIMD
+#define RNS_ROWS_DEEP_FROM 1024u
+#endif
+
 namespace rns {
 
 // The packed form's kernels (separate instantiations, so the explicit-descriptor
@@ -28,9 +32,6 @@ int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
     // round 3's stream kernel).
     const bool tiny = (sh.variant & ~16u) == 3u && sh.G == 4u && sh.U == 1u;
     if (a.align_mask >= 15u && !tiny) {
-#ifndef RNS_ROWS_DEEP_FROM  // typical lengths from this take D = 16 rows in flight at 4 waves/SIMD
-#define RNS_ROWS_DEEP_FROM 1024u
-#endif
         constexpr bool NT = RNS_STREAM_NT != 0;
         const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);
         if (a.len_hint >= RNS_ROWS_DEEP_FROM) {
@@ -78,6 +79,27 @@ int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
             hipLaunchKernelGGL((csum_rounds_kernel<4, 1, false, true, false, 1, true>), grid, block, 0, st, a);
     } else {
         return RNS_E_INVALID;
+    }
+    return hip_status(hipGetLastError());
+}
+
+// Transmit fill of a packed arena (align_log2 >= 4): the rows kernel in fill mode, D by the
+// typical length as for the plain checksum.
+int launch_fill_packed(const CsumArgs &a, hipStream_t st)
+{
+    constexpr bool NT = RNS_STREAM_NT != 0;
+    const bool buf = buf_records(a) < kOobOffset;
+    const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);
+    if (a.len_hint >= RNS_ROWS_DEEP_FROM) {
+        if (buf)
+            hipLaunchKernelGGL((csum_rows_kernel<NT, true, 16, true>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_rows_kernel<NT, false, 16, true>), grid, block, 0, st, a);
+    } else {
+        if (buf)
+            hipLaunchKernelGGL((csum_rows_kernel<NT, true, 8, true>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_rows_kernel<NT, false, 8, true>), grid, block, 0, st, a);
     }
     return hip_status(hipGetLastError());
 }

@@ -298,6 +298,33 @@ int rns_csum_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_
                        static_cast<hipStream_t>(stream));
 }
 
+int rns_csum_fill_packed_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_blk_off, const uint16_t *d_len16,
+                             uint32_t align_log2, const uint16_t *d_seed, const uint16_t *d_field, uint32_t field_off,
+                             uint16_t *d_out, uint32_t n, uint32_t flags, uint32_t len_hint, uint32_t *d_bad,
+                             void *stream)
+{
+    if (n == 0)
+        return RNS_OK;
+    if (!d_arena || !d_blk_off || !d_len16 || align_log2 < 4 || align_log2 > 12)
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    CsumArgs a{};
+    set_arena(a, d_arena, arena_bytes);
+    a.len16 = d_len16;
+    a.blk_off = d_blk_off;
+    a.align_mask = (1u << align_log2) - 1u;
+    a.seed = d_seed;
+    a.out = d_out;
+    a.bad = d_bad;
+    a.n = n;
+    a.flags = flags;
+    a.field = d_field;
+    a.field_off = field_off;
+    a.len_hint = len_hint;
+    return launch_fill_packed(a, static_cast<hipStream_t>(stream));
+}
+
 static uint32_t be_sum(const uint8_t *p, int nbytes)
 {
     uint32_t s = 0;

@@ -2171,8 +2171,18 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
 // (c3 isolated 230.2-231.0 -> 227.8-227.9 us; IMIX 445.6-447.6 -> 454-456, so IMIX keeps 8;
 // D = 12 at 5 waves/SIMD in between; two or four 64-packet sets per wave slower on IMIX:
 // session r04g).
-template <bool NT, bool BUF, int D>
-__global__ __launch_bounds__(64, D >= 16 ? 4 : 8) void csum_rows_kernel(const CsumArgs a)
+//
+// FILL (transmit in-place fill of a packed arena, rns_csum_fill_packed_dev): the field
+// (2 bytes at packet offset field[p] / field_off) counts as zero (buf.rs:286-288) and
+// receives the result big-endian (tcp.rs:970-973).  The owner loads the 32-byte sector
+// around its field with its end chunk, takes the field's bytes out of the row sum, and
+// rewrites the whole sector when it lies inside the packet (a full-sector write: no
+// read-modify-write at the memory side), else stores the two bytes.
+#ifndef RNS_ROWS_FILL_OCC  // waves/SIMD bound of the fill form at D = 8 (8 spills its sector registers)
+#define RNS_ROWS_FILL_OCC 6
+#endif
+template <bool NT, bool BUF, int D, bool FILL = false>
+__global__ __launch_bounds__(64, D >= 16 ? 4 : FILL ? RNS_ROWS_FILL_OCC : 8) void csum_rows_kernel(const CsumArgs a)
 {
     const uint32_t lane = threadIdx.x;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -2197,6 +2207,39 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : 8) void csum_rows_kernel(const Cs
     const uint32_t incl = wave_incl_scan(pad);
     const uint32_t excl = incl - pad;
     const uint32_t total = __builtin_amdgcn_readlane(incl, 63);  // the region's bytes
+    const uint64_t start = r0 + excl;
+    const bool ok = start <= a.arena_bytes && len <= a.arena_bytes - start;
+    // transmit fill: the field, the 32-byte sector around it (a.arena is 16-aligned; the
+    // sector's alignment is absolute) and whether that sector lies inside the packet
+    uint32_t fo = 0;
+    if constexpr (FILL)
+        fo = a.field ? static_cast<uint32_t>(a.field[q]) : a.field_off;
+    const bool fok = FILL && live && ok && fo + 2u <= len;
+    const uint64_t fpos = start + fo, fch = fpos & ~15ull;
+    const bool sec_back = ((static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a.arena) >> 4) +
+                            static_cast<uint32_t>(fch >> 4)) & 1u) != 0;
+    const uint64_t sec = fch - (sec_back ? 16u : 0u);
+    const bool sec_ok = fok && (fch >= 16u || !sec_back) && sec + 32u <= recs;
+    const uint32_t rel = static_cast<uint32_t>(fpos - sec);  // the field's first byte in the sector
+    uint4 sv0 = make_uint4(0, 0, 0, 0), sv1 = sv0;
+    uint32_t fb0 = 0, fb1 = 0;  // the field's bytes when the sector does not hold both
+    if constexpr (FILL) {
+        if constexpr (BUF) {
+            const uint32_t o = sec_ok ? static_cast<uint32_t>(sec) : kOobOffset;
+            const u32x4 x0 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, 0);
+            const u32x4 x1 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o + (sec_ok ? 16u : 0u), 0, 0);
+            sv0 = make_uint4(x0.x, x0.y, x0.z, x0.w);
+            sv1 = make_uint4(x1.x, x1.y, x1.z, x1.w);
+        } else if (sec_ok) {
+            sv0 = load_chunk<false>(a.arena + sec);
+            sv1 = load_chunk<false>(a.arena + sec + 16);
+        }
+        if (fok && (!sec_ok || rel == 31u)) {  // rare: odd field at a sector end, or the arena's first chunk
+            fb0 = a.arena[fpos];
+            fb1 = a.arena[fpos + 1];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
     uint32_t mine = 0;
     bool odd = false;
     if ((r0 & 15) == 0) {
@@ -2305,10 +2348,43 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : 8) void csum_rows_kernel(const Cs
         }
         odd = r0 & 1;  // every packet of the range shares the region start's misalignment
     }
-    const uint64_t start = r0 + excl;
-    const bool ok = start <= a.arena_bytes && len <= a.arena_bytes - start;
-    const uint16_t res = finalize_bits(mine, odd, false, seed, ok, a.flags);
-    if (live) {
+    if constexpr (FILL) {
+        // the field's bytes out of the sum (LE words pair bytes by absolute parity)
+        const uint32_t w[8] = {sv0.x, sv0.y, sv0.z, sv0.w, sv1.x, sv1.y, sv1.z, sv1.w};
+        uint32_t b0 = fb0, b1 = fb1;
+        if (sec_ok && rel != 31u) {
+            uint32_t d0 = 0, d1 = 0;
+#pragma unroll
+            for (uint32_t d = 0; d < 8; ++d) {
+                d0 = (rel >> 2) == d ? w[d] : d0;
+                d1 = ((rel + 1u) >> 2) == d ? w[d] : d1;
+            }
+            b0 = (d0 >> ((rel & 3u) * 8u)) & 0xffu;
+            b1 = (d1 >> (((rel + 1u) & 3u) * 8u)) & 0xffu;
+        }
+        mine -= fok ? (b0 << ((fpos & 1) * 8)) + (b1 << (((fpos + 1) & 1) * 8)) : 0u;
+    }
+    const uint16_t res = finalize_bits(mine, odd, false, seed, ok && (!FILL || fok), a.flags);
+    if constexpr (FILL) {
+        // set_be16(&mut packet[fo..fo + 2], result)
+        const uint32_t hi = static_cast<uint32_t>(res) >> 8, lo = static_cast<uint32_t>(res) & 0xffu;
+        uint8_t *arena_w = const_cast<uint8_t *>(a.arena);
+        if (sec_ok && rel != 31u && sec >= start && sec + 32u <= start + len) {
+            uint32_t w[8] = {sv0.x, sv0.y, sv0.z, sv0.w, sv1.x, sv1.y, sv1.z, sv1.w};
+#pragma unroll
+            for (uint32_t d = 0; d < 8; ++d) {
+                const uint32_t s0 = (rel & 3u) * 8u, s1 = ((rel + 1u) & 3u) * 8u;
+                w[d] = (rel >> 2) == d ? (w[d] & ~(0xffu << s0)) | (hi << s0) : w[d];
+                w[d] = ((rel + 1u) >> 2) == d ? (w[d] & ~(0xffu << s1)) | (lo << s1) : w[d];
+            }
+            store_block(reinterpret_cast<uint4 *>(arena_w + sec), make_uint4(w[0], w[1], w[2], w[3]));
+            store_block(reinterpret_cast<uint4 *>(arena_w + sec + 16), make_uint4(w[4], w[5], w[6], w[7]));
+        } else if (fok) {
+            arena_w[fpos] = static_cast<uint8_t>(hi);
+            arena_w[fpos + 1] = static_cast<uint8_t>(lo);
+        }
+    }
+    if (live && (!FILL || a.out)) {
         if (a.n < (1u << 30)) {  // buffer store, sc0|sc1 (the stream kernel's measured best, r03o)
             const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
                 static_cast<void *>(a.out), static_cast<short>(0), static_cast<int>(2u * a.n), 0x00020000);
@@ -2318,7 +2394,7 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : 8) void csum_rows_kernel(const Cs
         }
     }
     if (a.bad) {
-        const uint64_t rejected = __ballot(live && !ok);
+        const uint64_t rejected = __ballot(live && !(ok && (!FILL || fok)));
         if (rejected && lane == 0)
             atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
     }

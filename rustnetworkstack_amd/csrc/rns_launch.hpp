@@ -72,6 +72,7 @@ extern template int dispatch<false>(const CsumArgs &, uint32_t, uint32_t, uint32
 extern template int dispatch<true>(const CsumArgs &, uint32_t, uint32_t, uint32_t, uint32_t, hipStream_t);
 // k_packed.hip
 int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st);
+int launch_fill_packed(const CsumArgs &a, hipStream_t st);
 int launch_stream_rx(const CsumArgs &a, hipStream_t st);
 // k_chain.hip: K packets per lane (1..kChainMaxK)
 int launch_chain(const CsumArgs &a, uint32_t K, bool nt, bool runs, hipStream_t st);

@@ -63,6 +63,8 @@ def test_batch_calls_fail_loudly_without_gpu():
     assert lib.rns_host_ctx_create(0, 1 << 20, 2, ctypes.byref(p)) == _lib.RNS_E_NODEVICE
     assert lib.rns_fill_splitmix64_dev(fake, 64, 1, None) == _lib.RNS_E_NODEVICE
     assert lib.rns_csum_fill_dev(fake, 64, fake, fake, None, None, 0, None, 1, 0, None, None) == _lib.RNS_E_NODEVICE
+    assert lib.rns_csum_fill_packed_dev(fake, 64, fake, fake, 4, None, None, 16, None, 1, 0, 0, None,
+                                        None) == _lib.RNS_E_NODEVICE
     assert lib.rns_rx_verify_dev(fake, 64, fake, fake, 1, fake, fake, fake, None, None) == _lib.RNS_E_NODEVICE
     assert lib.rns_tx_fill_dev(fake, 64, fake, fake, 1, None, None) == _lib.RNS_E_NODEVICE
 

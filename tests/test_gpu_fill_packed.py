@@ -1,0 +1,127 @@
+"""Transmit in-place fill of a packed arena (rns_csum_fill_packed_dev): the same per-packet
+result and stores as rns_csum_fill_dev (tcp.rs:957-973, udp.rs:158-171, icmp.rs:87-112,
+ip.rs:158-159: the field counted as zero — buf.rs:286-288 — and the checksum stored
+big-endian into it), with the packed form's descriptors.  Bit-exact against the oracle;
+every other byte of the arena unchanged; filled packets pass the receive check."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from rustnetworkstack_amd import _lib
+from rustnetworkstack_amd.batch import csum_batch_packed, csum_fill_packed, packed_layout
+from rustnetworkstack_amd.workloads import make_layout
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def dev(a, view):
+    return torch.from_numpy(np.ascontiguousarray(a).view(view)).to(DEV)
+
+
+def host_u16(t):
+    torch.cuda.synchronize()
+    return t.view(torch.int16).cpu().numpy().view(np.uint16)
+
+
+def expected(oracle, arena_np, off, ln, seeds, field, base=0):
+    """Zero each field (alloc_header), 0xffff ^ ones_comp(seed, packet); packets whose
+    field does not fit get 0 and are not touched."""
+    a = arena_np.copy()
+    fits = field.astype(np.int64) + 2 <= ln.astype(np.int64)
+    for o, f, ok in zip(off, field, fits):
+        if ok:
+            a[base + int(o) + int(f)] = 0
+            a[base + int(o) + int(f) + 1] = 0
+    want = oracle.batch(a[base:], off, ln.astype(np.uint32), seeds, complement=True)
+    want[~fits] = 0
+    return want, fits
+
+
+def check_fill(oracle, ln, field, align_log2=4, first_off=0, base=0, seed_salt=1, len_hint=0, field_arg=True):
+    ln = np.asarray(ln, dtype=np.uint16)
+    n = ln.size
+    blk, off, end = packed_layout(ln, align_log2, first_off)
+    arena_np = O.splitmix64_bytes(0xF111 + seed_salt, base + end + 64)   # arbitrary prior field contents
+    seeds = (O.splitmix64_words(0x5EED + seed_salt, n) & np.uint64(0xFFFF)).astype(np.uint16)
+    field = np.asarray(field, dtype=np.uint16)
+    want, fits = expected(oracle, arena_np, off, ln, seeds, field, base)
+    full = torch.from_numpy(arena_np.copy()).to(DEV)
+    arena = full[base:]                                                 # base > 0: a misaligned arena pointer
+    out = torch.empty(n, dtype=torch.uint16, device=DEV)
+    bad = torch.zeros(1, dtype=torch.int32, device=DEV)
+    csum_fill_packed(arena, dev(blk.astype(np.uint64), np.int64), dev(ln, np.int16), dev(seeds, np.int16),
+                     align_log2=align_log2, field=dev(field, np.int16) if field_arg else None,
+                     field_off=int(field[0]) if n else 16, out=out, len_hint=len_hint, bad=bad)
+    got = full.cpu().numpy()
+    assert np.array_equal(host_u16(out), want), np.flatnonzero(host_u16(out) != want)[:5]
+    assert int(bad.item()) == int((~fits).sum())
+    idx = base + off.astype(np.int64) + field.astype(np.int64)
+    stored = (got[idx].astype(np.uint16) << 8) | got[idx + 1].astype(np.uint16)
+    assert np.array_equal(stored[fits], want[fits])
+    mask = np.ones(got.shape[0], dtype=bool)                             # nothing else changed
+    mask[idx[fits]] = False
+    mask[idx[fits] + 1] = False
+    assert np.array_equal(got[mask], arena_np[mask])
+    # the receive check (tcp.rs:838-850 form: sum with the stored field == 0 after complement)
+    rx = host_u16(csum_batch_packed(arena, dev(blk.astype(np.uint64), np.int64), dev(ln, np.int16),
+                                    dev(seeds, np.int16), align_log2=align_log2, complement=True))
+    word = fits & (field % 2 == 0)                                       # a field at an odd offset is
+    assert np.all(rx[word] == 0)                                         # not a word of the packet
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu_present():
+    if not torch.cuda.is_available() or _lib.load().rns_device_count() == 0:
+        pytest.fail("gpu tests need a GPU (the HIP path has no CPU fallback)")
+
+
+def test_mtu_tcp_fill(oracle):
+    """1500-byte TCP segments, field [16..18], the deep (D = 16) form."""
+    n = 64 * 300 + 5
+    check_fill(oracle, np.full(n, 1500), np.full(n, 16), len_hint=1500, field_arg=False)
+
+
+@pytest.mark.parametrize("align_log2", [4, 5, 6, 11])
+def test_imix_mixed_fields(oracle, align_log2):
+    """IMIX lengths, per-packet field offsets 2 / 6 / 10 / 16 (ICMP / UDP / IPv4 / TCP) and
+    odd ones (a field straddling a sector or chunk boundary), at several alignments."""
+    n = 40000
+    lay = make_layout("c5_imix", n=n)
+    w = O.splitmix64_words(0xF1E1D + align_log2, n)
+    field = np.array([2, 6, 10, 16, 3, 17, 15, 31], dtype=np.uint16)[(w >> np.uint64(8)) % np.uint64(8)]
+    check_fill(oracle, lay.length, field, align_log2=align_log2, seed_salt=align_log2, len_hint=350)
+
+
+@pytest.mark.parametrize("base,first_off", [(0, 16), (8, 0), (1, 32), (16, 0)])
+def test_arena_offsets(oracle, base, first_off):
+    """A first packet past the arena start and arena pointers at any alignment (a
+    misaligned pointer takes the wave-per-packet path; the sector rule is absolute)."""
+    n = 64 * 20 + 3
+    ln = (O.splitmix64_words(0xA11 + base, n) % np.uint64(700)).astype(np.uint16) + 20
+    check_fill(oracle, ln, np.full(n, 16), first_off=first_off, base=base, seed_salt=base)
+
+
+def test_short_empty_and_longest(oracle):
+    """Packets too short for their field (and empty ones) are rejected and untouched;
+    65535-byte packets and fields at the packet's last two bytes are filled."""
+    ln = np.array([0, 17, 18, 1, 65535, 40, 2, 3, 65535, 64] * 13, dtype=np.uint16)
+    field = np.array([16, 16, 16, 0, 65533, 38, 0, 2, 16, 62] * 13, dtype=np.uint16)
+    check_fill(oracle, ln, field, len_hint=1000)
+
+
+def test_tiny_packets(oracle):
+    """64-byte segments (the ACK case): many packets per row."""
+    n = 64 * 512 + 9
+    check_fill(oracle, np.full(n, 64), np.full(n, 16), len_hint=64, field_arg=False)
+
+
+def test_misaligned_packing_is_invalid():
+    arena = torch.zeros(256, dtype=torch.uint8, device=DEV)
+    with pytest.raises(ValueError):
+        csum_fill_packed(arena, torch.zeros(1, dtype=torch.int64, device=DEV),
+                         torch.full((4,), 40, dtype=torch.int16, device=DEV), align_log2=3)
+    st = _lib.load().rns_csum_fill_packed_dev(arena.data_ptr(), 256, arena.data_ptr(), arena.data_ptr(), 3, None,
+                                              None, 16, None, 4, 0, 0, None, None)
+    assert st == _lib.RNS_E_INVALID

@@ -5,6 +5,7 @@ batch checksum, on the headline batch (2^20 x 1500 B) and on IMIX:
 * chain    — rns_csum_chain_dev: every packet as the stack receives it after the
              IP trim, three fragments [492, 512, 496]
 * fill     — rns_csum_fill_dev: transmit fill of the TCP checksum field [16..18]
+* fill_packed — rns_csum_fill_packed_dev: the same fill with the packed descriptors
 * verify   — rns_rx_verify_dev: IPv4 header + TCP checks of whole datagrams
 * tx       — rns_tx_fill_dev: IPv4 header + TCP checksums of whole datagrams stored in
              place, pseudo-headers formed on the device
@@ -25,7 +26,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from rustnetworkstack_amd.batch import (PreparedBatch, csum_chain, csum_fill, rx_verify, tx_fill)  # noqa: E402
+from rustnetworkstack_amd.batch import (PreparedBatch, csum_chain, csum_fill, csum_fill_packed,  # noqa: E402
+                                        packed_layout, rx_verify, tx_fill)
 from rustnetworkstack_amd.workloads import DeviceBatch, make_layout  # noqa: E402
 
 L4 = bytes([192, 168, 1, 2])
@@ -107,6 +109,14 @@ def main():
         if "fill" in ops:
             ms = timed(lambda: csum_fill(b.arena, b.off, b.length, b.seed, field_off=16), args.steps, args.rounds)
             r["fill"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1)}
+        if "fill_packed" in ops:
+            blk, _, _ = packed_layout(lay.length, align_log2=4)
+            blk_t = torch.from_numpy(blk.view(np.int64)).to(dev)
+            len16 = torch.from_numpy(lay.length.astype(np.uint16).view(np.int16)).to(dev)
+            hint = int(round(lay.mean_len))
+            ms = timed(lambda: csum_fill_packed(b.arena, blk_t, len16, b.seed, align_log2=4, field_off=16,
+                                                len_hint=hint), args.steps, args.rounds)
+            r["fill_packed"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1)}
         if "tx" in ops:
             write_ipv4_tcp_headers(b, lay, dev)
             st = torch.empty(n, dtype=torch.uint8, device=dev)
