@@ -2181,6 +2181,18 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
 #ifndef RNS_ROWS_FILL_OCC  // waves/SIMD bound of the fill form at D = 8 (8 spills its sector registers)
 #define RNS_ROWS_FILL_OCC 6
 #endif
+#ifndef RNS_ROWS_FILL_BLOCK  // bytes of the aligned block around the field the fill loads and rewrites
+#define RNS_ROWS_FILL_BLOCK 32
+#endif
+#ifndef RNS_ROWS_FILL_AUX  // >= 0: the block stores as buffer stores with these cache-policy bits
+#define RNS_ROWS_FILL_AUX -1
+#endif
+#ifndef RNS_ROWS_FILL_STORE  // 1: rewrite the block around the field; 2: store the field's two bytes
+#define RNS_ROWS_FILL_STORE 1
+#endif
+#if RNS_ROWS_FILL_STORE == 0 && !defined(RNS_DIAGNOSTIC_BUILD)
+#error "RNS_ROWS_FILL_STORE=0 (no field stores) gives wrong results: diagnostic builds only"
+#endif
 template <bool NT, bool BUF, int D, bool FILL = false>
 __global__ __launch_bounds__(64, D >= 16 ? 4 : FILL ? RNS_ROWS_FILL_OCC : 8) void csum_rows_kernel(const CsumArgs a)
 {
@@ -2209,32 +2221,33 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : FILL ? RNS_ROWS_FILL_OCC : 8) voi
     const uint32_t total = __builtin_amdgcn_readlane(incl, 63);  // the region's bytes
     const uint64_t start = r0 + excl;
     const bool ok = start <= a.arena_bytes && len <= a.arena_bytes - start;
-    // transmit fill: the field, the 32-byte sector around it (a.arena is 16-aligned; the
-    // sector's alignment is absolute) and whether that sector lies inside the packet
+    // transmit fill: the field, the aligned block of FB bytes around it (a.arena is 16-aligned;
+    // the block's alignment is absolute) and whether it lies inside the packet
+    constexpr uint32_t FB = FILL ? RNS_ROWS_FILL_BLOCK : 16u, FC = FB / 16u;
     uint32_t fo = 0;
     if constexpr (FILL)
         fo = a.field ? static_cast<uint32_t>(a.field[q]) : a.field_off;
     const bool fok = FILL && live && ok && fo + 2u <= len;
     const uint64_t fpos = start + fo, fch = fpos & ~15ull;
-    const bool sec_back = ((static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a.arena) >> 4) +
-                            static_cast<uint32_t>(fch >> 4)) & 1u) != 0;
-    const uint64_t sec = fch - (sec_back ? 16u : 0u);
-    const bool sec_ok = fok && (fch >= 16u || !sec_back) && sec + 32u <= recs;
-    const uint32_t rel = static_cast<uint32_t>(fpos - sec);  // the field's first byte in the sector
-    uint4 sv0 = make_uint4(0, 0, 0, 0), sv1 = sv0;
-    uint32_t fb0 = 0, fb1 = 0;  // the field's bytes when the sector does not hold both
+    const uint32_t back = ((static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a.arena) >> 4) +
+                            static_cast<uint32_t>(fch >> 4)) & (FC - 1u)) * 16u;
+    const uint64_t sec = fch - back;
+    const bool sec_ok = fok && fch >= back && sec + FB <= recs;
+    const uint32_t rel = static_cast<uint32_t>(fpos - sec);  // the field's first byte in the block
+    uint4 sv[FC];
+    uint32_t fb0 = 0, fb1 = 0;  // the field's bytes when the block does not hold both
     if constexpr (FILL) {
-        if constexpr (BUF) {
-            const uint32_t o = sec_ok ? static_cast<uint32_t>(sec) : kOobOffset;
-            const u32x4 x0 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, 0);
-            const u32x4 x1 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o + (sec_ok ? 16u : 0u), 0, 0);
-            sv0 = make_uint4(x0.x, x0.y, x0.z, x0.w);
-            sv1 = make_uint4(x1.x, x1.y, x1.z, x1.w);
-        } else if (sec_ok) {
-            sv0 = load_chunk<false>(a.arena + sec);
-            sv1 = load_chunk<false>(a.arena + sec + 16);
+#pragma unroll
+        for (uint32_t i = 0; i < FC; ++i) {
+            if constexpr (BUF) {
+                const uint32_t o = sec_ok ? static_cast<uint32_t>(sec) + 16u * i : kOobOffset;
+                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, 0);
+                sv[i] = make_uint4(x.x, x.y, x.z, x.w);
+            } else {
+                sv[i] = sec_ok ? load_chunk<false>(a.arena + sec + 16u * i) : make_uint4(0, 0, 0, 0);
+            }
         }
-        if (fok && (!sec_ok || rel == 31u)) {  // rare: odd field at a sector end, or the arena's first chunk
+        if (fok && (!sec_ok || rel == FB - 1u)) {  // rare: odd field at a block end, or the arena's first chunk
             fb0 = a.arena[fpos];
             fb1 = a.arena[fpos + 1];
         }
@@ -2350,12 +2363,19 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : FILL ? RNS_ROWS_FILL_OCC : 8) voi
     }
     if constexpr (FILL) {
         // the field's bytes out of the sum (LE words pair bytes by absolute parity)
-        const uint32_t w[8] = {sv0.x, sv0.y, sv0.z, sv0.w, sv1.x, sv1.y, sv1.z, sv1.w};
+        uint32_t w[4 * FC];
+#pragma unroll
+        for (uint32_t i = 0; i < FC; ++i) {
+            w[4 * i] = sv[i].x;
+            w[4 * i + 1] = sv[i].y;
+            w[4 * i + 2] = sv[i].z;
+            w[4 * i + 3] = sv[i].w;
+        }
         uint32_t b0 = fb0, b1 = fb1;
-        if (sec_ok && rel != 31u) {
+        if (sec_ok && rel != FB - 1u) {
             uint32_t d0 = 0, d1 = 0;
 #pragma unroll
-            for (uint32_t d = 0; d < 8; ++d) {
+            for (uint32_t d = 0; d < 4 * FC; ++d) {
                 d0 = (rel >> 2) == d ? w[d] : d0;
                 d1 = ((rel + 1u) >> 2) == d ? w[d] : d1;
             }
@@ -2363,27 +2383,52 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : FILL ? RNS_ROWS_FILL_OCC : 8) voi
             b1 = (d1 >> (((rel + 1u) & 3u) * 8u)) & 0xffu;
         }
         mine -= fok ? (b0 << ((fpos & 1) * 8)) + (b1 << (((fpos + 1) & 1) * 8)) : 0u;
-    }
-    const uint16_t res = finalize_bits(mine, odd, false, seed, ok && (!FILL || fok), a.flags);
-    if constexpr (FILL) {
-        // set_be16(&mut packet[fo..fo + 2], result)
-        const uint32_t hi = static_cast<uint32_t>(res) >> 8, lo = static_cast<uint32_t>(res) & 0xffu;
+        const uint16_t r = finalize_bits(mine, odd, false, seed, ok && fok, a.flags);
+        // set_be16(&mut packet[fo..fo + 2], result): rewrite the largest aligned block (FB, ..., 32
+        // bytes) around the field that lies inside the packet, else store the two bytes
+        const uint32_t hi = static_cast<uint32_t>(r) >> 8, lo = static_cast<uint32_t>(r) & 0xffu;
         uint8_t *arena_w = const_cast<uint8_t *>(a.arena);
-        if (sec_ok && rel != 31u && sec >= start && sec + 32u <= start + len) {
-            uint32_t w[8] = {sv0.x, sv0.y, sv0.z, sv0.w, sv1.x, sv1.y, sv1.z, sv1.w};
+        uint32_t wsz = 0;  // bytes of the block rewritten
 #pragma unroll
-            for (uint32_t d = 0; d < 8; ++d) {
+        for (uint32_t bs = 32; bs <= FB; bs *= 2) {
+            const uint64_t bb = sec + (rel & ~(bs - 1u));
+            wsz = sec_ok && (rel & (bs - 1u)) != bs - 1u && bb >= start && bb + bs <= start + len ? bs : wsz;
+        }
+        if (RNS_ROWS_FILL_STORE == 0) {
+        } else if (RNS_ROWS_FILL_STORE == 1 && wsz) {
+#pragma unroll
+            for (uint32_t d = 0; d < 4 * FC; ++d) {
                 const uint32_t s0 = (rel & 3u) * 8u, s1 = ((rel + 1u) & 3u) * 8u;
                 w[d] = (rel >> 2) == d ? (w[d] & ~(0xffu << s0)) | (hi << s0) : w[d];
                 w[d] = ((rel + 1u) >> 2) == d ? (w[d] & ~(0xffu << s1)) | (lo << s1) : w[d];
             }
-            store_block(reinterpret_cast<uint4 *>(arena_w + sec), make_uint4(w[0], w[1], w[2], w[3]));
-            store_block(reinterpret_cast<uint4 *>(arena_w + sec + 16), make_uint4(w[4], w[5], w[6], w[7]));
+            const uint32_t c_lo = (rel & ~(wsz - 1u)) >> 4, c_hi = c_lo + (wsz >> 4);
+#pragma unroll
+            for (uint32_t i = 0; i < FC; ++i) {
+                if (i >= c_lo && i < c_hi) {
+                    if constexpr (BUF && RNS_ROWS_FILL_AUX >= 0) {
+                        const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+                            static_cast<void *>(arena_w), static_cast<short>(0), static_cast<int>(buf_records(a)),
+                            0x00020000);
+                        u32x4 x;
+                        x.x = w[4 * i];
+                        x.y = w[4 * i + 1];
+                        x.z = w[4 * i + 2];
+                        x.w = w[4 * i + 3];
+                        __builtin_amdgcn_raw_buffer_store_b128(x, wr, static_cast<uint32_t>(sec) + 16u * i, 0,
+                                                               RNS_ROWS_FILL_AUX);
+                    } else {
+                        store_block(reinterpret_cast<uint4 *>(arena_w + sec + 16u * i),
+                                    make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
+                    }
+                }
+            }
         } else if (fok) {
             arena_w[fpos] = static_cast<uint8_t>(hi);
             arena_w[fpos + 1] = static_cast<uint8_t>(lo);
         }
     }
+    const uint16_t res = finalize_bits(mine, odd, false, seed, ok && (!FILL || fok), a.flags);
     if (live && (!FILL || a.out)) {
         if (a.n < (1u << 30)) {  // buffer store, sc0|sc1 (the stream kernel's measured best, r03o)
             const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(

@@ -123,6 +123,46 @@ static int test_packed(hipStream_t st)
     for (uint32_t i = 0; i < n; ++i)
         CHECK(got[i] == (i < n - 5 ? want[i] : 0u), "short arena packet %u: %04x", i, got[i]);
     CHECK(bad == 5, "short arena: d_bad = %u (want 5)", bad);
+    /* rns_csum_fill_packed_dev: the TCP field [16..18] counted as zero and the result stored
+     * big-endian into it (tcp.rs:957-973); packets shorter than 18 bytes rejected, untouched */
+    uint32_t short_pkts = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (len16[i] < 18) {
+            want[i] = 0;
+            ++short_pkts;
+            continue;
+        }
+        uint8_t *f = arena + off[i] + 16;
+        const uint8_t f0 = f[0], f1 = f[1];
+        f[0] = f[1] = 0;
+        want[i] = (uint16_t)(0xffffu ^ (uint32_t)oracle_compute_ones_comp(seed[i], arena + off[i], len16[i]));
+        f[0] = f0;
+        f[1] = f1;
+    }
+    HIP_OK(hipMemset(d_bad, 0, sizeof *d_bad));
+    CHECK(rns_csum_fill_packed_dev(d_arena, bytes, d_blk, d_len16, 4, d_seed, NULL, 16, d_out, n, RNS_FLAG_COMPLEMENT,
+                                   340u, d_bad, st) == RNS_OK, "rns_csum_fill_packed_dev");
+    HIP_OK(hipStreamSynchronize(st));
+    HIP_OK(hipMemcpy(got, d_out, n * sizeof *got, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(&bad, d_bad, sizeof bad, hipMemcpyDeviceToHost));
+    uint8_t *back = malloc(bytes);
+    HIP_OK(hipMemcpy(back, d_arena, bytes, hipMemcpyDeviceToHost));
+    uint64_t changed = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        CHECK(got[i] == want[i], "packed fill packet %u (len %u): %04x != %04x", i, len16[i], got[i], want[i]);
+        if (len16[i] >= 18) {
+            const uint8_t *f = back + off[i] + 16;
+            CHECK(f[0] == (want[i] >> 8) && f[1] == (want[i] & 0xff), "packed fill packet %u: field %02x%02x", i,
+                  f[0], f[1]);
+            arena[off[i] + 16] = f[0];
+            arena[off[i] + 17] = f[1];
+        }
+    }
+    for (uint64_t b = 0; b < bytes; ++b)
+        changed += back[b] != arena[b];
+    CHECK(changed == 0, "packed fill: %llu bytes outside the fields changed", (unsigned long long)changed);
+    CHECK(bad == short_pkts, "packed fill: d_bad = %u (want %u)", bad, short_pkts);
+    free(back);
     hipFree(d_arena); hipFree(d_blk); hipFree(d_len16); hipFree(d_seed); hipFree(d_out); hipFree(d_bad);
     free(len16); free(seed); free(want); free(got); free(off); free(blk); free(len32); free(arena);
     return 0;
