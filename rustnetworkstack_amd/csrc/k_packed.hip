@@ -30,7 +30,10 @@ int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
     // 344.4-345.1 vs 346.4-347.1 (group kernel, u32 offsets), IMIX 451-453 vs 456 (round 3's
     // stream kernel).  Tiny packets keep the rounds kernel (c2: 13.2-13.7 vs 14.0-14.8 us with
     // round 3's stream kernel).
-    const bool tiny = (sh.variant & ~16u) == 3u && sh.G == 4u && sh.U == 1u;
+#ifndef RNS_PACKED_TINY_ROUNDS  // A/B knob: 0 = tiny packets through the rows kernel too
+#define RNS_PACKED_TINY_ROUNDS 1
+#endif
+    const bool tiny = RNS_PACKED_TINY_ROUNDS && (sh.variant & ~16u) == 3u && sh.G == 4u && sh.U == 1u;
     if (a.align_mask >= 15u && !tiny) {
         constexpr bool NT = RNS_STREAM_NT != 0;
         const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);

@@ -2148,6 +2148,93 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
     }
 }
 
+// The rows decomposition over one region that starts 16-byte aligned at r0 (an offset from
+// a.arena) and spans nrows KiB rows: the lane's packet covers chunks c0..e of the region (its
+// start 16-byte aligned, len bytes, len 0: none).  Returns the packet's LE word sum (pairs by
+// absolute parity).  csum_rows_kernel's aligned path and the chain kernel's runs (below).
+template <bool NT, bool BUF, int D>
+__device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __amdgpu_buffer_rsrc_t rsrc, uint64_t recs,
+                                                   uint64_t r0, uint32_t nrows, uint32_t c0, uint32_t e, uint32_t len)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    // the end chunk, first: its line is then an L2 hit for the row that streams it, if it is
+    // still there (pulling it from its row instead, four ds_bpermute per row, measured 2x
+    // slower: session r04g)
+    uint4 endv;
+    {
+        const uint64_t off = r0 + (static_cast<uint64_t>(e) << 4);
+        const bool in = len != 0 && off + 16 <= recs;
+        if constexpr (BUF) {
+            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, in ? static_cast<uint32_t>(off) : kOobOffset,
+                                                                  0, 0);
+            endv = make_uint4(x.x, x.y, x.z, x.w);
+        } else {
+            const uint4 x = load_chunk<false>(a.arena + (in ? off : 0));
+            endv = in ? x : make_uint4(0, 0, 0, 0);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t vlane = lane << 4;
+    uint4 v[D];
+    auto issue = [&](uint32_t k, uint4 &dst) {  // row k: chunk 64k + lane of the region
+        if constexpr (BUF) {
+            // wave-uniform row base (a row past the region: out of range, no traffic)
+            const uint32_t sb = k < nrows ? static_cast<uint32_t>(r0) + (k << 10) : kOobOffset;
+            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, sb + vlane, 0, NT ? kNtAux : 0);
+            dst = make_uint4(x.x, x.y, x.z, x.w);
+        } else {
+            const uint64_t off = r0 + (static_cast<uint64_t>(k) << 10) + vlane;
+            const bool in = k < nrows && off + 16 <= recs;
+            const uint4 x = load_chunk<NT>(a.arena + (in ? off : 0));
+            dst = in ? x : make_uint4(0, 0, 0, 0);
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        issue(j, v[j]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // the owner's partial end chunk (its padding bytes never count)
+    uint32_t part = 0;
+    if (len) {
+        const uint4 x = keep_first(endv, ((len - 1) & 15u) + 1u);
+        part = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
+        part = __builtin_amdgcn_sad_u16(x.y, 0, part);
+        part = __builtin_amdgcn_sad_u16(x.z, 0, part);
+        part = __builtin_amdgcn_sad_u16(x.w, 0, part);
+    }
+    // capture points: P(c0 - 1) and P(e - 1) (row, source lane); e == c0 takes the
+    // start's point twice (the difference is 0), c0 == 0 never captures (P(-1) = 0)
+    const uint32_t ca = c0 - 1u;
+    const uint32_t cb = e > c0 ? e - 1u : ca;
+    const uint32_t row_a = c0 ? ca >> 6 : 0xFFFFFFFFu, row_b = (e > c0 || c0) ? cb >> 6 : 0xFFFFFFFFu;
+    const int src_a = static_cast<int>((ca & 63u) << 2), src_b = static_cast<int>((cb & 63u) << 2);
+    uint32_t pa = 0, pb = 0, carry = 0;
+    for (uint32_t k0 = 0; k0 < nrows; k0 += D) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const uint32_t k = k0 + j;
+            const uint4 x = v[j];
+            uint32_t s = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
+            s = __builtin_amdgcn_sad_u16(x.y, 0, s);
+            s = __builtin_amdgcn_sad_u16(x.z, 0, s);
+            s = __builtin_amdgcn_sad_u16(x.w, 0, s);
+            // the row D ahead into the registers this row just freed (issued after the row
+            // is consumed: no loop-carried copy, exact vmcnt(D-1) waits)
+            __builtin_amdgcn_sched_barrier(0);
+            issue(k + D, v[j]);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t inc = wave_incl_scan(s);
+            const uint32_t ta = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_a, static_cast<int>(inc)));
+            const uint32_t tb = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_b, static_cast<int>(inc)));
+            pa = row_a == k ? carry + ta : pa;
+            pb = row_b == k ? carry + tb : pb;
+            carry += __builtin_amdgcn_readlane(inc, 63);
+        }
+    }
+    return len ? pb - pa + part : 0u;
+}
+
 // ---------------------------------------------------------------------------
 // Row stream with owner captures (round 4; the packed form's plain checksum for
 // 16-byte-aligned packets of a typical length 113-1200 B: IMIX).
@@ -2259,82 +2346,7 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : FILL ? RNS_ROWS_FILL_OCC : 8) voi
         const uint32_t nrows = (total + 1023) >> 10;
         const uint32_t c0 = excl >> 4;
         const uint32_t e = len ? (excl + len - 1) >> 4 : c0;
-        // the end chunk, first: its line is then an L2 hit for the row that streams it, if it is
-        // still there (pulling it from its row instead, four ds_bpermute per row, measured 2x
-        // slower: session r04g)
-        uint4 endv;
-        {
-            const uint64_t off = r0 + (static_cast<uint64_t>(e) << 4);
-            const bool in = len != 0 && off + 16 <= recs;
-            if constexpr (BUF) {
-                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, in ? static_cast<uint32_t>(off) : kOobOffset,
-                                                                      0, 0);
-                endv = make_uint4(x.x, x.y, x.z, x.w);
-            } else {
-                const uint4 x = load_chunk<false>(a.arena + (in ? off : 0));
-                endv = in ? x : make_uint4(0, 0, 0, 0);
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        const uint32_t vlane = lane << 4;
-        uint4 v[D];
-        auto issue = [&](uint32_t k, uint4 &dst) {  // row k: chunk 64k + lane of the region
-            if constexpr (BUF) {
-                // wave-uniform row base (a row past the region: out of range, no traffic)
-                const uint32_t sb = k < nrows ? static_cast<uint32_t>(r0) + (k << 10) : kOobOffset;
-                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, sb + vlane, 0, NT ? kNtAux : 0);
-                dst = make_uint4(x.x, x.y, x.z, x.w);
-            } else {
-                const uint64_t off = r0 + (static_cast<uint64_t>(k) << 10) + vlane;
-                const bool in = k < nrows && off + 16 <= recs;
-                const uint4 x = load_chunk<NT>(a.arena + (in ? off : 0));
-                dst = in ? x : make_uint4(0, 0, 0, 0);
-            }
-        };
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-            issue(j, v[j]);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // the owner's partial end chunk (its padding bytes never count)
-        uint32_t part = 0;
-        if (len) {
-            const uint4 x = keep_first(endv, ((len - 1) & 15u) + 1u);
-            part = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
-            part = __builtin_amdgcn_sad_u16(x.y, 0, part);
-            part = __builtin_amdgcn_sad_u16(x.z, 0, part);
-            part = __builtin_amdgcn_sad_u16(x.w, 0, part);
-        }
-        // capture points: P(c0 - 1) and P(e - 1) (row, source lane); e == c0 takes the
-        // start's point twice (the difference is 0), c0 == 0 never captures (P(-1) = 0)
-        const uint32_t ca = c0 - 1u;
-        const uint32_t cb = e > c0 ? e - 1u : ca;
-        const uint32_t row_a = c0 ? ca >> 6 : 0xFFFFFFFFu, row_b = (e > c0 || c0) ? cb >> 6 : 0xFFFFFFFFu;
-        const int src_a = static_cast<int>((ca & 63u) << 2), src_b = static_cast<int>((cb & 63u) << 2);
-        uint32_t pa = 0, pb = 0, carry = 0;
-        for (uint32_t k0 = 0; k0 < nrows; k0 += D) {
-#pragma unroll
-            for (int j = 0; j < D; ++j) {
-                const uint32_t k = k0 + j;
-                const uint4 x = v[j];
-                uint32_t s = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
-                s = __builtin_amdgcn_sad_u16(x.y, 0, s);
-                s = __builtin_amdgcn_sad_u16(x.z, 0, s);
-                s = __builtin_amdgcn_sad_u16(x.w, 0, s);
-                // the row D ahead into the registers this row just freed (issued after the row
-                // is consumed: no loop-carried copy, exact vmcnt(D-1) waits)
-                __builtin_amdgcn_sched_barrier(0);
-                issue(k + D, v[j]);
-                __builtin_amdgcn_sched_barrier(0);
-                const uint32_t inc = wave_incl_scan(s);
-                const uint32_t ta = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_a, static_cast<int>(inc)));
-                const uint32_t tb = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_b, static_cast<int>(inc)));
-                pa = row_a == k ? carry + ta : pa;
-                pb = row_b == k ? carry + tb : pb;
-                carry += __builtin_amdgcn_readlane(inc, 63);
-            }
-        }
-        mine = len ? pb - pa + part : 0u;
+        mine = rows_region_sum<NT, BUF, D>(a, rsrc, recs, r0, nrows, c0, e, len);
     } else {
         // ---- unaligned region (rare): the whole wave sums one packet at a time ----
         const uint64_t start = r0 + excl;

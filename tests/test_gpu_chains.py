@@ -372,3 +372,45 @@ def test_runs_by_packet(oracle, break_every, max_len):
             got = run_chain(torch.from_numpy(arena_np).to(DEV), offs, lens, first, seeds, complement=complement,
                             runs=runs)
             assert np.array_equal(got, expect)
+
+
+@pytest.mark.parametrize("max_gap,max_len,align", [(0, 1600, 16), (15, 1600, 16), (48, 700, 16), (0, 20_000, 16),
+                                                   (0, 1600, 2), (600, 100, 16)])
+def test_runs_tiling_a_region(oracle, max_gap, max_len, align):
+    """RNS_FLAG_CHAIN_RUNS with runs that tile the arena (csum_rows_kernel's decomposition
+    over 64 runs: 16-byte-aligned starts, ascending, gaps within a quarter of the bytes):
+    0-4 adjacent fragments per packet (all but the last even, empty ones included, packets
+    without fragments), gaps of 0..max_gap bytes rounded up to `align`.  align 2 / large gaps:
+    waves fall back to the class pass.  Both against the oracle, with and without the flag."""
+    n = 40_000 if max_len <= 1600 else 4_000
+    w = O.splitmix64_words(0x7111 + max_gap + max_len + align, n)
+    nfr = (w % np.uint64(5)).astype(np.int64)
+    first = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(nfr, out=first[1:])
+    nf = int(first[-1])
+    fw = O.splitmix64_words(0x7112 + max_len, nf)
+    lens = (fw % np.uint64(max_len // 2 + 1)).astype(np.int64)
+    last = np.zeros(nf, dtype=bool)
+    last[first[1:][nfr > 0] - 1] = True
+    lens[~last] &= ~1
+    lens[(fw >> np.uint64(40)) % np.uint64(30) == 0] = 0
+    offs = np.zeros(nf, dtype=np.int64)
+    pos = 64
+    gaps = ((w >> np.uint64(20)) % np.uint64(max_gap + 1)).astype(np.int64)
+    for p in range(n):
+        pos = (pos + int(gaps[p]) + align - 1) // align * align
+        for f in range(int(first[p]), int(first[p + 1])):
+            offs[f] = pos
+            pos += int(lens[f])
+    size = pos + 4096
+    arena_np = O.splitmix64_bytes(0x7113 + max_len, size)
+    seeds = (w >> np.uint64(40) & np.uint64(0xFFFF)).astype(np.uint16)
+    offs, lens, first = offs.astype(np.uint64), lens.astype(np.uint32), first.astype(np.uint32)
+    a = torch.from_numpy(arena_np).to(DEV)
+    for complement in (False, True):
+        expect = oracle.chain_batch(arena_np, offs, lens, first, seeds, complement=complement)
+        for runs in (False, True):
+            for hint in (0, 300):
+                got = host_u16(csum_chain(a, dev(offs, np.int64), dev(lens, np.int32), dev(first, np.int32),
+                                          dev(seeds, np.int16), complement=complement, frag_len_hint=hint, runs=runs))
+                assert np.array_equal(got, expect), (complement, runs, hint, int(np.flatnonzero(got != expect)[0]))
