@@ -2148,6 +2148,9 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
     }
 }
 
+#ifndef RNS_ROWS_END_LATE  // A/B knob: the owner's end-chunk load issued with its row, not up front
+#define RNS_ROWS_END_LATE 0
+#endif
 // The rows decomposition over one region that starts 16-byte aligned at r0 (an offset from
 // a.arena) and spans nrows KiB rows: the lane's packet covers chunks c0..e of the region (its
 // start 16-byte aligned, len bytes, len 0: none).  Returns the packet's LE word sum (pairs by
@@ -2160,8 +2163,22 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
     // the end chunk, first: its line is then an L2 hit for the row that streams it, if it is
     // still there (pulling it from its row instead, four ds_bpermute per row, measured 2x
     // slower: session r04g)
-    uint4 endv;
-    {
+    uint4 endv = make_uint4(0, 0, 0, 0);
+    constexpr bool kLate = BUF && RNS_ROWS_END_LATE != 0;
+    const uint32_t row_e = len ? e >> 6 : 0xFFFFFFFFu;
+    // RNS_ROWS_END_LATE: the owners load their end chunks a group of D rows ahead of the rows
+    // that hold them (one exec-masked load per group: its line is then still in L2 when the row
+    // streams it), not all before the first row
+    auto load_end_late = [&](uint32_t k) {  // end chunks in rows [k, k + D)
+        if constexpr (kLate) {
+            if (row_e - k < static_cast<uint32_t>(D)) {
+                const uint32_t off = static_cast<uint32_t>(r0) + (e << 4);
+                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16u <= recs ? off : kOobOffset, 0, 0);
+                endv = make_uint4(x.x, x.y, x.z, x.w);
+            }
+        }
+    };
+    if constexpr (!kLate) {
         const uint64_t off = r0 + (static_cast<uint64_t>(e) << 4);
         const bool in = len != 0 && off + 16 <= recs;
         if constexpr (BUF) {
@@ -2189,20 +2206,25 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
             dst = in ? x : make_uint4(0, 0, 0, 0);
         }
     };
+    load_end_late(0);
 #pragma unroll
     for (int j = 0; j < D; ++j) {
         issue(j, v[j]);
         __builtin_amdgcn_sched_barrier(0);
     }
     // the owner's partial end chunk (its padding bytes never count)
-    uint32_t part = 0;
-    if (len) {
-        const uint4 x = keep_first(endv, ((len - 1) & 15u) + 1u);
-        part = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
-        part = __builtin_amdgcn_sad_u16(x.y, 0, part);
-        part = __builtin_amdgcn_sad_u16(x.z, 0, part);
-        part = __builtin_amdgcn_sad_u16(x.w, 0, part);
-    }
+    auto end_part = [&]() -> uint32_t {
+        uint32_t part = 0;
+        if (len) {
+            const uint4 x = keep_first(endv, ((len - 1) & 15u) + 1u);
+            part = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
+            part = __builtin_amdgcn_sad_u16(x.y, 0, part);
+            part = __builtin_amdgcn_sad_u16(x.z, 0, part);
+            part = __builtin_amdgcn_sad_u16(x.w, 0, part);
+        }
+        return part;
+    };
+    uint32_t part = kLate ? 0u : end_part();
     // capture points: P(c0 - 1) and P(e - 1) (row, source lane); e == c0 takes the
     // start's point twice (the difference is 0), c0 == 0 never captures (P(-1) = 0)
     const uint32_t ca = c0 - 1u;
@@ -2211,6 +2233,7 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
     const int src_a = static_cast<int>((ca & 63u) << 2), src_b = static_cast<int>((cb & 63u) << 2);
     uint32_t pa = 0, pb = 0, carry = 0;
     for (uint32_t k0 = 0; k0 < nrows; k0 += D) {
+        load_end_late(k0 + D);  // (the rows this group issues)
 #pragma unroll
         for (int j = 0; j < D; ++j) {
             const uint32_t k = k0 + j;
@@ -2232,6 +2255,8 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
             carry += __builtin_amdgcn_readlane(inc, 63);
         }
     }
+    if constexpr (kLate)
+        part = end_part();
     return len ? pb - pa + part : 0u;
 }
 
