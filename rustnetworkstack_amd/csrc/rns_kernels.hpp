@@ -2148,17 +2148,21 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
     }
 }
 
-#ifndef RNS_ROWS_END_LATE  // A/B knob: the owner's end-chunk load issued with its row, not up front
-#define RNS_ROWS_END_LATE 0
+#ifndef RNS_ROWS_END_LATE  // the owner's end-chunk load issued a group of rows ahead of its row, not up
+#define RNS_ROWS_END_LATE 1  // front (c3 isolated 228.2-229.4 -> 224.8 us, traffic 1.030 -> 1.006x; session r04q)
+#endif
+#ifndef RNS_ROWS_TAIL_MASK  // A/B knob: lanes past the region's end in its last row load nothing
+#define RNS_ROWS_TAIL_MASK 0
 #endif
 // The rows decomposition over one region that starts 16-byte aligned at r0 (an offset from
-// a.arena) and spans nrows KiB rows: the lane's packet covers chunks c0..e of the region (its
+// a.arena) and holds total bytes (a multiple of 16; ceil(total / 1 KiB) rows): the lane's packet covers chunks c0..e of the region (its
 // start 16-byte aligned, len bytes, len 0: none).  Returns the packet's LE word sum (pairs by
 // absolute parity).  csum_rows_kernel's aligned path and the chain kernel's runs (below).
 template <bool NT, bool BUF, int D>
 __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __amdgpu_buffer_rsrc_t rsrc, uint64_t recs,
-                                                   uint64_t r0, uint32_t nrows, uint32_t c0, uint32_t e, uint32_t len)
+                                                   uint64_t r0, uint32_t total, uint32_t c0, uint32_t e, uint32_t len)
 {
+    const uint32_t nrows = (total + 1023) >> 10;
     const uint32_t lane = threadIdx.x & 63u;
     // the end chunk, first: its line is then an L2 hit for the row that streams it, if it is
     // still there (pulling it from its row instead, four ds_bpermute per row, measured 2x
@@ -2196,8 +2200,16 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
     auto issue = [&](uint32_t k, uint4 &dst) {  // row k: chunk 64k + lane of the region
         if constexpr (BUF) {
             // wave-uniform row base (a row past the region: out of range, no traffic)
-            const uint32_t sb = k < nrows ? static_cast<uint32_t>(r0) + (k << 10) : kOobOffset;
-            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, sb + vlane, 0, NT ? kNtAux : 0);
+            uint32_t o;
+            if constexpr (RNS_ROWS_TAIL_MASK != 0) {
+                // lanes past the region's end load nothing (the next unit's wave streams those
+                // bytes, often on another XCD's L2)
+                const uint32_t rel = (k << 10) + vlane;
+                o = rel < total ? static_cast<uint32_t>(r0) + rel : kOobOffset;
+            } else {
+                o = (k < nrows ? static_cast<uint32_t>(r0) + (k << 10) : kOobOffset) + vlane;
+            }
+            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, NT ? kNtAux : 0);
             dst = make_uint4(x.x, x.y, x.z, x.w);
         } else {
             const uint64_t off = r0 + (static_cast<uint64_t>(k) << 10) + vlane;
@@ -2368,10 +2380,9 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : FILL ? RNS_ROWS_FILL_OCC : 8) voi
     uint32_t mine = 0;
     bool odd = false;
     if ((r0 & 15) == 0) {
-        const uint32_t nrows = (total + 1023) >> 10;
         const uint32_t c0 = excl >> 4;
         const uint32_t e = len ? (excl + len - 1) >> 4 : c0;
-        mine = rows_region_sum<NT, BUF, D>(a, rsrc, recs, r0, nrows, c0, e, len);
+        mine = rows_region_sum<NT, BUF, D>(a, rsrc, recs, r0, total, c0, e, len);
     } else {
         // ---- unaligned region (rare): the whole wave sums one packet at a time ----
         const uint64_t start = r0 + excl;
