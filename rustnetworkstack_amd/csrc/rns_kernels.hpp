@@ -2151,8 +2151,8 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
 #ifndef RNS_ROWS_END_LATE  // the owner's end-chunk load issued a group of rows ahead of its row, not up
 #define RNS_ROWS_END_LATE 1  // front (c3 isolated 228.2-229.4 -> 224.8 us, traffic 1.030 -> 1.006x; session r04q)
 #endif
-#ifndef RNS_ROWS_TAIL_MASK  // A/B knob: lanes past the region's end in its last row load nothing
-#define RNS_ROWS_TAIL_MASK 0
+#ifndef RNS_ROWS_TAIL_MASK  // lanes past the region's end in its last row load nothing (IMIX isolated
+#define RNS_ROWS_TAIL_MASK 1  // 451.7-453.3 -> 447.9-448.4 us, traffic 1.062 -> 1.042x; session r04r)
 #endif
 // The rows decomposition over one region that starts 16-byte aligned at r0 (an offset from
 // a.arena) and holds total bytes (a multiple of 16; ceil(total / 1 KiB) rows): the lane's packet covers chunks c0..e of the region (its
