@@ -2151,6 +2151,9 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
 #ifndef RNS_ROWS_END_LATE  // the owner's end-chunk load issued a group of rows ahead of its row, not up
 #define RNS_ROWS_END_LATE 1  // front (c3 isolated 228.2-229.4 -> 224.8 us, traffic 1.030 -> 1.006x; session r04q)
 #endif
+#ifndef RNS_ROWS_LINE_ALIGN  // A/B knob: rows start at the 128-byte line below the region
+#define RNS_ROWS_LINE_ALIGN 0
+#endif
 #ifndef RNS_ROWS_TAIL_MASK  // lanes past the region's end in its last row load nothing (IMIX isolated
 #define RNS_ROWS_TAIL_MASK 1  // 451.7-453.3 -> 447.9-448.4 us, traffic 1.062 -> 1.042x; session r04r)
 #endif
@@ -2162,6 +2165,17 @@ template <bool NT, bool BUF, int D>
 __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __amdgpu_buffer_rsrc_t rsrc, uint64_t recs,
                                                    uint64_t r0, uint32_t total, uint32_t c0, uint32_t e, uint32_t len)
 {
+    if constexpr (RNS_ROWS_LINE_ALIGN != 0) {
+        // start the row stream at the 128-byte line below the region (the few bytes before it
+        // belong to no packet of this unit; prefix differences cancel them), so every 1 KiB row
+        // covers 8 whole lines, not 9 — IMIX regions end anywhere on a 16-byte boundary
+        const uint32_t la = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a.arena) + r0) & 127u;  // absolute
+        const uint32_t lead = la <= r0 ? la : 0u;
+        r0 -= lead;
+        total += lead;
+        c0 += lead >> 4;
+        e += lead >> 4;
+    }
     const uint32_t nrows = (total + 1023) >> 10;
     const uint32_t lane = threadIdx.x & 63u;
     // the end chunk, first: its line is then an L2 hit for the row that streams it, if it is
