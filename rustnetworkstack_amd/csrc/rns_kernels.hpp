@@ -2151,8 +2151,8 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
 #ifndef RNS_ROWS_END_LATE  // the owner's end-chunk load issued a group of rows ahead of its row, not up
 #define RNS_ROWS_END_LATE 1  // front (c3 isolated 228.2-229.4 -> 224.8 us, traffic 1.030 -> 1.006x; session r04q)
 #endif
-#ifndef RNS_ROWS_LINE_ALIGN  // A/B knob: rows start at the 128-byte line below the region
-#define RNS_ROWS_LINE_ALIGN 0
+#ifndef RNS_ROWS_LINE_ALIGN  // rows start at the 128-byte line below the region (IMIX 445.8-446.0 ->
+#define RNS_ROWS_LINE_ALIGN 1  // 436.6-437.5 us, 0.809 -> 0.825, traffic 1.042 -> 1.034x; session r04w)
 #endif
 #ifndef RNS_ROWS_TAIL_MASK  // lanes past the region's end in its last row load nothing (IMIX isolated
 #define RNS_ROWS_TAIL_MASK 1  // 451.7-453.3 -> 447.9-448.4 us, traffic 1.062 -> 1.042x; session r04r)
