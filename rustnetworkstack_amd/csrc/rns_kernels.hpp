@@ -1904,6 +1904,9 @@ __device__ __forceinline__ uint4 keep_first(uint4 v, uint32_t c)
 #ifndef RNS_STREAM_D  // rows (1 KiB loads) in flight per wave
 #define RNS_STREAM_D 4
 #endif
+#ifndef RNS_STREAM_LINE_ALIGN  // A/B knob: receive verify's row stream from the 128-byte line below the region
+#define RNS_STREAM_LINE_ALIGN 0
+#endif
 #ifndef RNS_STREAM_RX_OCC  // waves/SIMD bound of the receive-verify instantiation (its finish needs registers)
 #define RNS_STREAM_RX_OCC 6
 #endif
@@ -2010,13 +2013,17 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
     }
     if ((r0 & 15) == 0) {
         // ---- stream path ----
-        const uint32_t nrows = (total + 1023) >> 10;
+        // (rows from the 128-byte line below the region, as csum_rows_kernel: RNS_ROWS_LINE_ALIGN)
+        const uint32_t la = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a.arena) + r0) & 127u;
+        const uint32_t lead = (RNS_STREAM_LINE_ALIGN != 0 && la <= r0) ? la : 0u;
+        const uint64_t rb = r0 - lead;
+        const uint32_t nrows = (total + lead + 1023) >> 10;
         tab[lane] = 0xFFFFFFFFu;  // tag 0x7FFF: never a row
         wave_lds_fence();
         uint32_t carry = 0;
         uint4 v[kStreamD];
         auto issue = [&](uint32_t k, uint4 &dst) {  // row k: chunk 64k + lane of the region
-            const uint64_t off = r0 + (static_cast<uint64_t>(k) << 10) + (lane << 4);
+            const uint64_t off = rb + (static_cast<uint64_t>(k) << 10) + (lane << 4);
             const bool in = k < nrows && off + 16 <= recs;
             if constexpr (BUF) {
                 const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(
@@ -2034,8 +2041,8 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
             issue(j, v[j]);
             __builtin_amdgcn_sched_barrier(0);
         }
-        const uint32_t c0 = excl >> 4;
-        const uint32_t e = (excl + len - 1) >> 4;
+        const uint32_t c0 = (excl + lead) >> 4;
+        const uint32_t e = (excl + lead + len - 1) >> 4;
         const uint32_t ent = (lane << 4) | ((len - 1) & 15u);
         const bool ne = len != 0;
         for (uint32_t k0 = 0; k0 < nrows; k0 += kStreamD) {
