@@ -1904,8 +1904,8 @@ __device__ __forceinline__ uint4 keep_first(uint4 v, uint32_t c)
 #ifndef RNS_STREAM_D  // rows (1 KiB loads) in flight per wave
 #define RNS_STREAM_D 4
 #endif
-#ifndef RNS_STREAM_LINE_ALIGN  // A/B knob: receive verify's row stream from the 128-byte line below the region
-#define RNS_STREAM_LINE_ALIGN 0
+#ifndef RNS_STREAM_LINE_ALIGN  // receive verify's row stream from the 128-byte line below the region
+#define RNS_STREAM_LINE_ALIGN 1    // (IMIX verify 473.6-473.7 -> 469.5-471.5 us, c3 equal; session r04y)
 #endif
 #ifndef RNS_STREAM_RX_OCC  // waves/SIMD bound of the receive-verify instantiation (its finish needs registers)
 #define RNS_STREAM_RX_OCC 6
