@@ -8,7 +8,8 @@ padding up to the next 2^align boundary), with P(c) the region's inclusive prefi
 (P(-1) = 0; e == c0: the end chunk alone), taken mod 2^32 with u32 prefixes that wrap, and the
 result finished as every kernel does (fold, byte swap for an even start, + seed, fold).  The
 model works a wave (64 packets) at a time with rows of 64 chunks, as the kernel does, so the
-capture rows/lanes are the kernel's.  Non-zero padding bytes, padding chunks (align 32..4096),
+capture rows/lanes are the kernel's — also with the row stream starting at the 128-byte line
+below each region (the kernel's default since round 4: the bytes before the region cancel).  Non-zero padding bytes, padding chunks (align 32..4096),
 empty packets, maximum lengths and all-0xff bytes (u32 prefix wrap) included."""
 import numpy as np
 import pytest
@@ -22,8 +23,10 @@ def fold(x):
     return x
 
 
-def rows_model(arena, blk_off, length, seed, complement=True):
-    """One 64-packet unit per 'wave'; returns the u16 results."""
+def rows_model(arena, blk_off, length, seed, complement=True, line=0):
+    """One 64-packet unit per 'wave'; returns the u16 results.  line = 128: the row stream
+    starts at the 128-byte line below the region (RNS_ROWS_LINE_ALIGN), so the prefix also
+    holds the bytes before the region — they cancel in every difference."""
     n = len(length)
     out = np.zeros(n, dtype=np.uint16)
     words = arena.view(np.uint16).astype(np.uint64)  # LE words at even offsets
@@ -37,9 +40,11 @@ def rows_model(arena, blk_off, length, seed, complement=True):
         pad = (ln + align - 1) // align * align
         excl = np.concatenate(([0], np.cumsum(pad)[:-1]))
         total = int(pad.sum())
-        nch = total // 16
-        c = chunk_sum[r0 // 16:r0 // 16 + nch]
+        lead = (r0 % line) if line else 0                  # bytes of the first line before the region
+        nch = (total + lead) // 16
+        c = chunk_sum[(r0 - lead) // 16:(r0 - lead) // 16 + nch]
         prefix = np.cumsum(c) & 0xFFFFFFFF                 # u32, wraps like the kernel's carry
+        excl = excl + lead
         for lane in range(m):
             L = int(ln[lane])
             if L == 0:
@@ -50,7 +55,7 @@ def rows_model(arena, blk_off, length, seed, complement=True):
                 pa = int(prefix[c0 - 1]) if c0 > 0 else 0
                 pb = int(prefix[e - 1]) if e > c0 else pa
                 nv = ((L - 1) & 15) + 1
-                endb = arena[r0 + 16 * e:r0 + 16 * e + nv].astype(np.uint64)
+                endb = arena[r0 - lead + 16 * e:r0 - lead + 16 * e + nv].astype(np.uint64)
                 part = int(endb[0::2].sum() + (endb[1::2].sum() << 8))
                 s = (pb - pa + part) & 0xFFFFFFFF
             x = fold(s)
@@ -89,8 +94,15 @@ def test_rows_decomposition_matches_oracle(oracle, align_log2, pattern):
     seed = rng.integers(0, 0x10000, n).astype(np.uint16)
     blk_off = off[::64].copy()
     got = rows_model(arena, blk_off, length, seed)
+    got_line = rows_model(arena, blk_off, length, seed, line=128)
+    # the same packets 48 bytes into the arena (garbage before them): the first region's line
+    # starts before its first packet too
+    arena48 = np.concatenate((O.splitmix64_bytes(0x48, 48), arena))
+    got_line48 = rows_model(arena48, blk_off + 48, length, seed, line=128)
     want = oracle.batch(arena, off, length.astype(np.uint32), seed, complement=True)
     # the oracle panics on empty slices (util.rs:92); the batch kernels return the seed
     empty = length == 0
     want[empty] = (seed[empty] ^ 0xFFFF).astype(np.uint16)
     assert np.array_equal(got, want), np.flatnonzero(got != want)[:5]
+    assert np.array_equal(got_line, want), np.flatnonzero(got_line != want)[:5]
+    assert np.array_equal(got_line48, want), np.flatnonzero(got_line48 != want)[:5]
