@@ -2185,9 +2185,8 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
     }
     const uint32_t nrows = (total + 1023) >> 10;
     const uint32_t lane = threadIdx.x & 63u;
-    // the end chunk, first: its line is then an L2 hit for the row that streams it, if it is
-    // still there (pulling it from its row instead, four ds_bpermute per row, measured 2x
-    // slower: session r04g)
+    // the owner's end chunk (pulling it from its row instead, four ds_bpermute per row, measured
+    // 2x slower: session r04g)
     uint4 endv = make_uint4(0, 0, 0, 0);
     constexpr bool kLate = BUF && RNS_ROWS_END_LATE != 0;
     const uint32_t row_e = len ? e >> 6 : 0xFFFFFFFFu;
@@ -2295,7 +2294,7 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
 
 // ---------------------------------------------------------------------------
 // Row stream with owner captures (round 4; the packed form's plain checksum for
-// 16-byte-aligned packets of a typical length 113-1200 B: IMIX).
+// 16-byte-aligned packets above the tiny class: c3, c4, IMIX).
 //
 // A wave owns 64 consecutive packets and streams their bytes as ONE region, row k =
 // the region's k-th KiB (64 lanes x 16 B), D rows in flight — as csum_stream_kernel,
@@ -2306,9 +2305,10 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
 //     sum_p = P(e - 1) - P(c0 - 1) + (the first ((len - 1) & 15) + 1 bytes of chunk e)
 // (P(-1) = 0; e == c0: the end chunk alone).  The owner lane pulls P(c0 - 1) and
 // P(e - 1) from the lanes that hold them with ds_bpermute in the rows they fall in, and
-// loads its end chunk itself once per unit (issued before the rows: the line is then
-// an L2 hit for the row that streams it), so the end chunk's padding bytes never need a
-// per-row mask.  Per KiB: 4 sad + the scan + two captures, no LDS memory, no fences
+// loads its end chunk itself one group of D rows before the row that streams it (the line
+// is fetched once: RNS_ROWS_END_LATE), so the end chunk's padding bytes never need a
+// per-row mask.  Rows start at the 128-byte line below the region (RNS_ROWS_LINE_ALIGN) and
+// lanes past its end load nothing (RNS_ROWS_TAIL_MASK).  Per KiB: 4 sad + the scan + two captures, no LDS memory, no fences
 // (csum_stream_kernel: a table publish, two wave fences, the masks; 57 VALU/KB).
 // u32 differences are exact: a packet's LE word sum is < 2^32.
 // ---------------------------------------------------------------------------
