@@ -103,6 +103,18 @@ def test_arena_offsets(oracle, base, first_off):
     check_fill(oracle, ln, np.full(n, 16), first_off=first_off, base=base, seed_salt=base)
 
 
+@pytest.mark.parametrize("base", [0, 8])
+def test_jumbo_hint(oracle, base):
+    """A jumbo-frame hint (two waves per 64-packet block when the build splits blocks) over
+    mixed lengths up to 12 000 bytes with empty and short packets, n not a multiple of 64."""
+    n = 64 * 40 + 37
+    ln = (O.splitmix64_words(0x1A2B + base, n) % np.uint64(12_000)).astype(np.uint16)
+    ln[::11] = 0
+    ln[5::13] = 17
+    field = np.array([16, 6, 2, 10], dtype=np.uint16)[np.arange(n) % 4]
+    check_fill(oracle, ln, field, base=base, seed_salt=7 + base, len_hint=9000)
+
+
 def test_short_empty_and_longest(oracle):
     """Packets too short for their field (and empty ones) are rejected and untouched;
     65535-byte packets and fields at the packet's last two bytes are filled."""

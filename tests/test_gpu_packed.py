@@ -145,7 +145,7 @@ def test_unaligned_regions(oracle, first_off, base_shift):
     big = torch.zeros(end + 16 + base_shift, dtype=torch.uint8, device=DEV)
     big[base_shift:].copy_(torch.from_numpy(arena))
     view = big[base_shift:]  # data_ptr() = base + base_shift
-    for hint in (64, 340, 1500):
+    for hint in (64, 340, 1500, 9000):
         got = host_u16(csum_batch_packed(view, dev(blk.astype(np.uint64), np.int64), dev(ln.astype(np.uint16), np.int16),
                                          dev(sd, np.int16), align_log2=4, complement=True, len_hint=hint))
         assert np.array_equal(got, expect), hint
