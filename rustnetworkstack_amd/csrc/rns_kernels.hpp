@@ -1732,7 +1732,12 @@ __global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(
     constexpr uint32_t kBad = 0x80000000u;
     const uint64_t per_wave = 64ull * K;
 
-    for (uint64_t base = static_cast<uint64_t>(wave) * per_wave; base < a.n; base += nwaves * per_wave) {
+    // (the packet index in 32 bits — a.n < 2^32 — with the step taken in 64 bits, so the loop
+    // cannot wrap: one VGPR less across the class pass)
+    const uint64_t first_pkt = static_cast<uint64_t>(wave) * per_wave, step = static_cast<uint64_t>(nwaves) * per_wave;
+    if (first_pkt >= a.n)
+        return;
+    for (uint32_t base = static_cast<uint32_t>(first_pkt);;) {
         uint32_t lo_all = 0xFFFFFFFFu, hi_all = 0u;
         bool runs_all = true;
         for (uint32_t q = 0; q < K; ++q) {
@@ -1763,16 +1768,16 @@ __global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(
         try_runs = by_packet;
         const uint32_t passes = by_packet ? K : (F1 - F0 + 63) / 64;  // (F1 >= F0, equal if no fragments)
         for (uint32_t it = 0; it < passes; ++it) {
-            const uint64_t fb = F0 + 64ull * it;
+            const uint32_t fb = F0 + 64u * it;  // < F1 <= n_frags: 32 bits
             uint64_t d_start = 0;
             uint32_t d_len = 0;
             if (by_packet) {
                 const uint32_t i = it * 64 + lane;
                 d_len = pk[RUNS ? 3 : 0][i];
                 d_start = pk[RUNS ? 4 : 0][i] - a.base_adjust;  // (base_adjust added back below)
-            } else if (fb + lane < F1) {
-                d_start = a.off[fb + lane];
-                d_len = a.len[fb + lane];
+            } else if (static_cast<uint64_t>(fb) + lane < F1) {
+                d_start = a.off[static_cast<uint64_t>(fb) + lane];
+                d_len = a.len[static_cast<uint64_t>(fb) + lane];
             }
             d_start += a.base_adjust;
             const bool d_ok = d_start <= a.arena_bytes && d_len <= a.arena_bytes - d_start;
@@ -1800,8 +1805,8 @@ __global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(
             // owner lanes: each packet's fragments inside [fb, fb + 64), in order
             for (uint32_t q = 0; q < K; ++q) {
                 const uint32_t i = q * 64 + lane;
-                uint64_t t = max(static_cast<uint64_t>(pk[0][i]), fb);
-                const uint64_t hi = min(static_cast<uint64_t>(pk[1][i]), fb + 64);
+                uint32_t t = max(pk[0][i], fb);
+                const uint32_t hi = static_cast<uint32_t>(min(static_cast<uint64_t>(pk[1][i]), static_cast<uint64_t>(fb) + 64));
                 if (!__ballot(t < hi))
                     continue;
                 uint32_t acc = pk[2][i];
@@ -1843,6 +1848,10 @@ __global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(
             }
         }
         wave_lds_fence();  // the next batch rewrites pk
+        const uint64_t next = static_cast<uint64_t>(base) + step;
+        if (next >= a.n)
+            break;
+        base = static_cast<uint32_t>(next);
     }
 }
 
