@@ -246,7 +246,10 @@ int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
     // Nontemporal loads for NetBuffer-sized fragments (c3 as 3 fragments: 298 -> 289 us
     // packed back to back, 281 -> 261 us in 512-byte buffers), not for IMIX's mix of
     // 40-byte packets and 512-byte fragments (646 -> 670 us): profiles/archive/r02/r02_chain_ab.json.
-    const bool nt = (frag_len_hint ? frag_len_hint : 512u) >= 384u;
+#ifndef RNS_CHAIN_NT_FROM  // fragment-length hints from this take the nontemporal instantiation
+#define RNS_CHAIN_NT_FROM 384u
+#endif
+    const bool nt = (frag_len_hint ? frag_len_hint : 512u) >= RNS_CHAIN_NT_FROM;
     // RNS_FLAG_CHAIN_RUNS: the run-checking kernel (buffer path; a hint, ignored otherwise)
     const bool runs = kChainRuns && (flags & RNS_FLAG_CHAIN_RUNS) && buf_records(a) < kOobOffset;
     return launch_chain(a, K, nt, runs, static_cast<hipStream_t>(stream));
