@@ -1910,8 +1910,8 @@ __device__ __forceinline__ uint4 keep_first(uint4 v, uint32_t c)
 #ifndef RNS_STREAM_NT  // nontemporal loads in the stream kernel
 #define RNS_STREAM_NT 1
 #endif
-#ifndef RNS_STREAM_D  // rows (1 KiB loads) in flight per wave
-#define RNS_STREAM_D 4
+#ifndef RNS_STREAM_D  // rows (1 KiB loads) in flight per wave (8 since the rows start line-aligned:
+#define RNS_STREAM_D 8   // IMIX verify 472.3-472.8 -> 468.0-470.3 us, c3 235.9 -> 234.5; 6: 476.9; r04af)
 #endif
 #ifndef RNS_STREAM_LINE_ALIGN  // receive verify's row stream from the 128-byte line below the region
 #define RNS_STREAM_LINE_ALIGN 1    // (IMIX verify 473.6-473.7 -> 469.5-471.5 us, c3 equal; session r04y)
