@@ -2338,15 +2338,8 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
 #ifndef RNS_ROWS_FILL_BLOCK  // bytes of the aligned block around the field the fill loads and rewrites
 #define RNS_ROWS_FILL_BLOCK 32
 #endif
-#ifndef RNS_ROWS_FILL_AUX  // >= 0: the block stores as buffer stores with these cache-policy bits
-#define RNS_ROWS_FILL_AUX -1
-#endif
-#ifndef RNS_ROWS_FILL_STORE  // 1: rewrite the block around the field; 2: store the field's two bytes
-#define RNS_ROWS_FILL_STORE 1
-#endif
-#if RNS_ROWS_FILL_STORE == 0 && !defined(RNS_DIAGNOSTIC_BUILD)
-#error "RNS_ROWS_FILL_STORE=0 (no field stores) gives wrong results: diagnostic builds only"
-#endif
+// (Two-byte stores, nontemporal and sc0|sc1 block stores were measured and cost the same or more:
+// profiles/r04_fill_store_ab.json.)
 template <bool NT, bool BUF, int D, bool FILL = false>
 __global__ __launch_bounds__(64, D >= 16 ? 4 : FILL ? RNS_ROWS_FILL_OCC : 8) void csum_rows_kernel(const CsumArgs a)
 {
@@ -2472,8 +2465,7 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : FILL ? RNS_ROWS_FILL_OCC : 8) voi
             const uint64_t bb = sec + (rel & ~(bs - 1u));
             wsz = sec_ok && (rel & (bs - 1u)) != bs - 1u && bb >= start && bb + bs <= start + len ? bs : wsz;
         }
-        if (RNS_ROWS_FILL_STORE == 0) {
-        } else if (RNS_ROWS_FILL_STORE == 1 && wsz) {
+        if (wsz) {
 #pragma unroll
             for (uint32_t d = 0; d < 4 * FC; ++d) {
                 const uint32_t s0 = (rel & 3u) * 8u, s1 = ((rel + 1u) & 3u) * 8u;
@@ -2482,25 +2474,10 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : FILL ? RNS_ROWS_FILL_OCC : 8) voi
             }
             const uint32_t c_lo = (rel & ~(wsz - 1u)) >> 4, c_hi = c_lo + (wsz >> 4);
 #pragma unroll
-            for (uint32_t i = 0; i < FC; ++i) {
-                if (i >= c_lo && i < c_hi) {
-                    if constexpr (BUF && RNS_ROWS_FILL_AUX >= 0) {
-                        const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-                            static_cast<void *>(arena_w), static_cast<short>(0), static_cast<int>(buf_records(a)),
-                            0x00020000);
-                        u32x4 x;
-                        x.x = w[4 * i];
-                        x.y = w[4 * i + 1];
-                        x.z = w[4 * i + 2];
-                        x.w = w[4 * i + 3];
-                        __builtin_amdgcn_raw_buffer_store_b128(x, wr, static_cast<uint32_t>(sec) + 16u * i, 0,
-                                                               RNS_ROWS_FILL_AUX);
-                    } else {
-                        store_block(reinterpret_cast<uint4 *>(arena_w + sec + 16u * i),
-                                    make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
-                    }
-                }
-            }
+            for (uint32_t i = 0; i < FC; ++i)
+                if (i >= c_lo && i < c_hi)
+                    store_block(reinterpret_cast<uint4 *>(arena_w + sec + 16u * i),
+                                make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
         } else if (fok) {
             arena_w[fpos] = static_cast<uint8_t>(hi);
             arena_w[fpos + 1] = static_cast<uint8_t>(lo);
