@@ -717,15 +717,12 @@ def launch_ranks(args, argv) -> int:
     GPU has been touched yet, but the child must own the ranks, not this process),
     relay its output and return its exit code.  The child sees WORLD_SIZE == N, so
     its main() runs the ranks' path."""
-    import socket
     import subprocess
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
     script = os.path.abspath(sys.argv[0]) if sys.argv and sys.argv[0].endswith(".py") else os.path.abspath(__file__)
+    # the c10d rendezvous on port 0: the launcher's own store picks a free port (no probe-then-
+    # release race with another process), on 127.0.0.1 (the hostname may not resolve)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr=127.0.0.1", f"--master-port={port}", script] + list(argv)
+           "--rdzv-backend=c10d", "--rdzv-endpoint=127.0.0.1:0", "--local-addr=127.0.0.1", script] + list(argv)
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     print(f"bench.py: --gpus {args.gpus} without WORLD_SIZE: launching {args.gpus} ranks via torch.distributed.run",
           file=sys.stderr, flush=True)

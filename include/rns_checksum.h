@@ -170,6 +170,28 @@ int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
                        const uint16_t *d_seed, uint16_t *d_out, uint32_t n_pkts, uint32_t flags,
                        uint32_t frag_len_hint, uint16_t *d_frag_sums, uint32_t *d_bad, void *stream);
 
+/* Transmit fill over fragment chains, the shape the reference actually transmits:
+ * tcp_output / udp_output / icmp_output_* (tcp.rs:957-973, udp.rs:158-171,
+ * icmp.rs:87-112) checksum a NetBuffer whose FIRST fragment is the head fragment
+ * alloc_header prepended (buf.rs:262-291, zero-filled, so the field counts as zero:
+ * buf.rs:286-288), then set_be16 the result into header_mut() = that fragment.  Packet i
+ * = the CSR chain of rns_csum_chain_dev; its field is at byte d_field[i] (NULL =>
+ * field_off for every packet: TCP 16, UDP 6, ICMP 2) of fragment d_first[i].  The chain
+ * is folded exactly as compute_buffer_ones_comp(d_seed[i], chain) with the field's two
+ * bytes counted as zero, and the result (0xffff ^ sum with RNS_FLAG_COMPLEMENT, as every
+ * call site stores it; UDP's 0 is stored as is) is stored big-endian into the field.
+ * d_out (optional) receives the results.  A packet with no fragments, a malformed range,
+ * a fragment outside the arena, or a head fragment too short for its field is left
+ * untouched, gets d_out 0 and is counted in *d_bad.  Fragments of different packets
+ * must not overlap a field.  RNS_FLAG_CHAIN_RUNS: the hint of rns_csum_chain_dev (the
+ * head fragment then starts each run).  Lay the head fragments of consecutive packets
+ * back to back in a header region (a batching transmit path's header arena): a wave's
+ * 64 field stores then land in a few cache lines instead of 64 scattered ones. */
+int rns_csum_chain_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_frag_off,
+                            const uint32_t *d_frag_len, uint32_t n_frags, const uint32_t *d_first,
+                            const uint16_t *d_seed, const uint16_t *d_field, uint32_t field_off, uint16_t *d_out,
+                            uint32_t n_pkts, uint32_t flags, uint32_t frag_len_hint, uint32_t *d_bad, void *stream);
+
 /* Transmit in-place fill (tcp.rs:957-973, udp.rs:158-171, icmp.rs:87-112,
  * ip.rs:158-159): for packet i, sum d_arena[d_off[i] .. + d_len[i]) seeded with
  * d_seed[i], counting the 2-byte checksum field at packet offset d_field[i]

@@ -50,6 +50,7 @@ EXPORTED_SYMBOLS = (
     "rns_csum_batch_strided_dev",
     "rns_csum_batch_dev_cfg",
     "rns_csum_chain_dev",
+    "rns_csum_chain_fill_dev",
     "rns_csum_fill_dev",
     "rns_csum_fill_packed_dev",
     "rns_rx_verify_dev",
@@ -122,6 +123,8 @@ _SIGNATURES = {
     "rns_csum_batch_strided_dev": (_int, [_vp, _u64, _u64, _u64, _u32, _vp, _vp, _u32, _u32, _vp, _vp]),
     "rns_csum_batch_dev_cfg": (_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _u32, _vp, _vp]),
     "rns_csum_chain_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp]),
+    "rns_csum_chain_fill_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp, _vp, _u32, _vp, _u32, _u32, _u32, _vp,
+                                       _vp]),
     "rns_csum_fill_dev": (_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u32, _vp, _u32, _u32, _vp, _vp]),
     "rns_csum_fill_packed_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp, _u32, _vp, _u32, _u32, _u32, _vp, _vp]),
     "rns_rx_verify_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),

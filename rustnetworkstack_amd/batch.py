@@ -348,6 +348,55 @@ def csum_chain(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch.Tens
     return out
 
 
+def csum_chain_fill(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch.Tensor, first: torch.Tensor,
+                    seed: torch.Tensor | None = None, *, field: torch.Tensor | None = None, field_off: int = 16,
+                    complement: bool = True, out: torch.Tensor | None = None, bad: torch.Tensor | None = None,
+                    frag_len_hint: int = 512, runs: bool = False) -> torch.Tensor | None:
+    """Transmit fill over fragment chains (rns_csum_chain_fill_dev): packet i = fragments
+    ``first[i] .. first[i+1]`` as for ``csum_chain``; its checksum field is at byte
+    ``field[i]`` (or ``field_off``) of its FIRST fragment (the head fragment
+    alloc_header prepended, buf.rs:262-291), counts as zero, and receives
+    ``compute_buffer_ones_comp(seed, chain) ^ 0xffff`` big-endian (tcp.rs:957-973).
+    Returns ``out`` if given."""
+    _require_cuda(arena, "arena", (torch.uint8,))
+    _require_cuda(frag_off, "frag_off", (torch.int64,))
+    _require_cuda(frag_len, "frag_len", (torch.int32,))
+    _require_cuda(first, "first", (torch.int32,))
+    nf = frag_off.numel()
+    n = first.numel() - 1
+    if frag_len.numel() != nf or n < 0:
+        raise ValueError("frag_off/frag_len sizes differ or first is empty")
+    if n >= 2 ** 32 or nf >= 2 ** 32:
+        raise ValueError("at most 2^32-1 packets and fragments per call")
+    dev = arena.device
+    for name, t in (("frag_off", frag_off), ("frag_len", frag_len), ("first", first)):
+        if t.device != dev:
+            raise ValueError(f"{name} is on {t.device}, arena on {dev}")
+    ptrs = []
+    for name, t in (("seed", seed), ("field", field), ("out", out)):
+        if t is None:
+            ptrs.append(None)
+            continue
+        _require_cuda(t, name, _U16)
+        if t.numel() != n or t.device != dev:
+            raise ValueError(f"{name} must have one entry per packet on the arena's device")
+        ptrs.append(t.data_ptr())
+    if field is None and not 0 <= int(field_off) < 2 ** 32:
+        raise ValueError("field_off must be a u32")
+    bad_ptr = None
+    if bad is not None:
+        _require_cuda(bad, "bad", (torch.int32,))
+        bad_ptr = bad.data_ptr()
+    flags = (_lib.RNS_FLAG_COMPLEMENT if complement else 0) | (_lib.RNS_FLAG_CHAIN_RUNS if runs else 0)
+    with torch.cuda.device(dev):
+        st = _lib.load().rns_csum_chain_fill_dev(arena.data_ptr(), arena.numel(), frag_off.data_ptr(),
+                                                 frag_len.data_ptr(), nf, first.data_ptr(), ptrs[0], ptrs[1],
+                                                 int(field_off), ptrs[2], n, flags, int(frag_len_hint), bad_ptr,
+                                                 _stream_handle(dev))
+    _lib.check(st, "rns_csum_chain_fill_dev")
+    return out
+
+
 def csum_fill(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, seed: torch.Tensor | None = None, *,
               field: torch.Tensor | None = None, field_off: int = 16, complement: bool = True,
               out: torch.Tensor | None = None, bad: torch.Tensor | None = None) -> torch.Tensor | None:
@@ -400,6 +449,10 @@ def csum_fill_packed(arena: torch.Tensor, blk_off: torch.Tensor, len16: torch.Te
         raise ValueError("blk_off must have one entry per 64 packets")
     if not 4 <= align_log2 <= 12:
         raise ValueError("the packed fill needs align_log2 in 4..12")
+    if field is None and not 0 <= int(field_off) <= 0xFFFD:
+        # packed lengths are u16: no packet can hold a field past byte 65533 (the C ABI itself
+        # rejects every packet of such a call and leaves the arena unchanged)
+        raise ValueError("field_off must be in 0..65533 for the packed form")
     dev = arena.device
     ptrs = []
     for name, t in (("blk_off", blk_off), ("len16", len16)):

@@ -206,25 +206,16 @@ int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uin
     return dispatch<true>(a, sh.variant, sh.G, sh.U, sh.max_blocks, static_cast<hipStream_t>(stream));
 }
 
-int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_frag_off,
-                       const uint32_t *d_frag_len, uint32_t n_frags, const uint32_t *d_first,
-                       const uint16_t *d_seed, uint16_t *d_out, uint32_t n_pkts, uint32_t flags,
-                       uint32_t frag_len_hint, uint16_t *d_frag_sums, uint32_t *d_bad, void *stream)
+}  // extern "C"
+
+// Fragment chains: the chain kernel's arguments and launch (checksum or head-fragment fill).
+template <bool FILL>
+static int chain_launch(CsumArgs &a, const uint64_t *d_frag_off, const uint32_t *d_frag_len, uint32_t n_frags,
+                        const uint32_t *d_first, uint32_t n_pkts, uint32_t flags, uint32_t frag_len_hint,
+                        hipStream_t stream)
 {
-    (void)d_frag_sums;  // scratch of the two-pass form (round 1); the one-pass kernel needs none
-    if (n_pkts == 0)
-        return RNS_OK;
-    if (!d_arena || !d_first || !d_out || (n_frags && (!d_frag_off || !d_frag_len)))
-        return RNS_E_INVALID;
-    if (int st = check_device())
-        return st;
-    CsumArgs a{};
-    set_arena(a, d_arena, arena_bytes);
     a.off = d_frag_off;
     a.len = d_frag_len;
-    a.seed = d_seed;
-    a.out = d_out;
-    a.bad = d_bad;
     a.n = n_pkts;
     a.flags = flags;
     a.first = d_first;
@@ -252,7 +243,52 @@ int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
     const bool nt = (frag_len_hint ? frag_len_hint : 512u) >= RNS_CHAIN_NT_FROM;
     // RNS_FLAG_CHAIN_RUNS: the run-checking kernel (buffer path; a hint, ignored otherwise)
     const bool runs = kChainRuns && (flags & RNS_FLAG_CHAIN_RUNS) && buf_records(a) < kOobOffset;
-    return launch_chain(a, K, nt, runs, static_cast<hipStream_t>(stream));
+    return launch_chain<FILL>(a, K, nt, runs, stream);
+}
+
+extern "C" {
+
+int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_frag_off,
+                       const uint32_t *d_frag_len, uint32_t n_frags, const uint32_t *d_first,
+                       const uint16_t *d_seed, uint16_t *d_out, uint32_t n_pkts, uint32_t flags,
+                       uint32_t frag_len_hint, uint16_t *d_frag_sums, uint32_t *d_bad, void *stream)
+{
+    (void)d_frag_sums;  // scratch of the two-pass form (round 1); the one-pass kernel needs none
+    if (n_pkts == 0)
+        return RNS_OK;
+    if (!d_arena || !d_first || !d_out || (n_frags && (!d_frag_off || !d_frag_len)))
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    CsumArgs a{};
+    set_arena(a, d_arena, arena_bytes);
+    a.seed = d_seed;
+    a.out = d_out;
+    a.bad = d_bad;
+    return chain_launch<false>(a, d_frag_off, d_frag_len, n_frags, d_first, n_pkts, flags, frag_len_hint,
+                               static_cast<hipStream_t>(stream));
+}
+
+int rns_csum_chain_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_frag_off,
+                            const uint32_t *d_frag_len, uint32_t n_frags, const uint32_t *d_first,
+                            const uint16_t *d_seed, const uint16_t *d_field, uint32_t field_off, uint16_t *d_out,
+                            uint32_t n_pkts, uint32_t flags, uint32_t frag_len_hint, uint32_t *d_bad, void *stream)
+{
+    if (n_pkts == 0)
+        return RNS_OK;
+    if (!d_arena || !d_first || (n_frags && (!d_frag_off || !d_frag_len)))
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    CsumArgs a{};
+    set_arena(a, d_arena, arena_bytes);
+    a.seed = d_seed;
+    a.out = d_out;
+    a.bad = d_bad;
+    a.field = d_field;
+    a.field_off = field_off;
+    return chain_launch<true>(a, d_frag_off, d_frag_len, n_frags, d_first, n_pkts, flags, frag_len_hint,
+                              static_cast<hipStream_t>(stream));
 }
 
 // Grid of the stash-mode kernels (one 64-datagram batch per one-wave workgroup).  Batches

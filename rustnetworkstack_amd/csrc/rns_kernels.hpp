@@ -1707,7 +1707,18 @@ __device__ __forceinline__ uint32_t fragment_run(const CsumArgs &a, uint32_t f0,
 constexpr int kChainBlock = RNS_CHAIN_BLOCK;
 // RUNS: the RNS_FLAG_CHAIN_RUNS instantiation (buffer path only).  A separate kernel:
 // compiled into the plain one, the run check cost it ~5 % (registers) even unused.
-template <bool NT, bool BUF, uint32_t KMAX, bool RUNS = false>
+//
+// FILL (rns_csum_chain_fill_dev, the transmit shape of tcp_output / udp_output /
+// icmp_output_*: tcp.rs:957-973, udp.rs:158-171, icmp.rs:87-112): the packet's checksum
+// field lies in its FIRST fragment (the head fragment alloc_header prepended, buf.rs:262-
+// 291), counts as zero (buf.rs:286-288), and receives the result big-endian (set_be16,
+// the header_mut() slice = the first fragment).  The owner loads the field's two bytes
+// with its descriptors and takes their contribution out of the head fragment's EXACT word
+// sum before it is folded (the lane that summed the fragment hands the raw sum over), so
+// zero sums fold exactly as the reference's; after the fold it stores the two bytes.  A
+// packet whose head fragment cannot hold its field (or has no fragments) is rejected:
+// result 0, counted, nothing stored.
+template <bool NT, bool BUF, uint32_t KMAX, bool RUNS = false, bool FILL = false>
 __global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(const CsumArgs a)
 {
     static_assert(!RUNS || BUF, "runs: buffer path only");
@@ -1717,7 +1728,9 @@ __global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(
     // of a 4-waves/SIMD budget): the fragment range and the running sum (bit 31 = a
     // bad descriptor seen).
     // RUNS: [3] the packet's run bytes (fragment_run), [4] its start
-    constexpr int kPk = RUNS ? 5 : 3;
+    // FILL: [kPk - 1] the field's contribution to the head fragment's raw sum
+    constexpr int kPk = (RUNS ? 5 : 3) + (FILL ? 1 : 0);
+    constexpr int kPf = kPk - 1;
     __shared__ uint32_t pk_lds[kChainBlock / 64][kPk][KMAX * 64];
     const uint32_t lane = threadIdx.x & 63;
     uint32_t (&pk)[kPk][KMAX * 64] = pk_lds[threadIdx.x >> 6];
@@ -1741,7 +1754,7 @@ __global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(
         uint32_t lo_all = 0xFFFFFFFFu, hi_all = 0u;
         bool runs_all = true;
         for (uint32_t q = 0; q < K; ++q) {
-            const uint64_t p = base + q * 64 + lane;
+            const uint64_t p = static_cast<uint64_t>(base) + q * 64 + lane;  // (widened before the add)
             const bool live = p < a.n;
             uint32_t f0 = live ? a.first[p] : 0u, f1 = live ? a.first[p + 1] : 0u;
             const bool ok = f0 <= f1 && f1 <= a.n_frags;
@@ -1752,7 +1765,27 @@ __global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(
             hi_all = f0 < f1 ? max(hi_all, f1) : hi_all;
             pk[0][q * 64 + lane] = f0;
             pk[1][q * 64 + lane] = f1;
-            pk[2][q * 64 + lane] = acc | (ok ? 0u : kBad);
+            bool fok = true;
+            if constexpr (FILL) {
+                // the field in the head fragment f0: its bytes' share of that fragment's raw sum
+                // (LE words paired by absolute parity; the exact BE words past 128 KiB)
+                uint32_t fc = 0;
+                fok = false;
+                if (ok && f0 < f1) {
+                    const uint64_t ho = a.off[f0] + a.base_adjust;
+                    const uint32_t hl = a.len[f0];
+                    const uint32_t fo = a.field ? static_cast<uint32_t>(a.field[p]) : a.field_off;
+                    fok = ho <= a.arena_bytes && hl <= a.arena_bytes - ho && fo <= hl && hl - fo >= 2u;
+                    if (fok) {
+                        const uint64_t fp = ho + fo;
+                        const uint32_t b0 = a.arena[fp], b1 = a.arena[fp + 1];
+                        fc = hl > kNoWrapBytes ? ((fo & 1u) ? b0 | (b1 << 8) : (b0 << 8) | b1)
+                                               : (b0 << ((fp & 1) * 8)) + (b1 << (((fp + 1) & 1) * 8));
+                    }
+                }
+                pk[kPf][q * 64 + lane] = fc;
+            }
+            pk[2][q * 64 + lane] = acc | (ok && fok ? 0u : kBad);
             if constexpr (RUNS) {
                 uint64_t rs = 0;
                 const uint32_t run = (ok && try_runs) ? fragment_run(a, f0, f1, rs) : kNoRun;
@@ -1794,12 +1827,17 @@ __global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(
                 const uint32_t x = fold16(w);
                 g = odd ? x : (((x & 0xff) << 8) | (x >> 8));
             }
-            const uint32_t gflag = (big ? 1u : 0u) | (d_ok ? 0u : 2u);
+            const uint32_t gflag = (big ? 1u : 0u) | (d_ok ? 0u : 2u) | (FILL && odd ? 4u : 0u);
             wave_lds_fence();
             if (by_packet) {  // the lane's packet is its run: one fold (never big, never bad)
                 const uint32_t i = it * 64 + lane;
-                const uint32_t s = (pk[2][i] & 0xffffu) + g;
-                pk[2][i] = (s & 0xffff) + (s >> 16);
+                uint32_t gr = g;
+                if constexpr (FILL) {  // the run starts with the head fragment: the field out of it
+                    const uint32_t x = fold16(w - pk[kPf][i]);
+                    gr = odd ? x : (((x & 0xff) << 8) | (x >> 8));
+                }
+                const uint32_t s = (pk[2][i] & 0xffffu) + gr;
+                pk[2][i] = ((s & 0xffff) + (s >> 16)) | (FILL ? pk[2][i] & kBad : 0u);
                 continue;
             }
             // owner lanes: each packet's fragments inside [fb, fb + 64), in order
@@ -1810,11 +1848,17 @@ __global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(
                 if (!__ballot(t < hi))
                     continue;
                 uint32_t acc = pk[2][i];
+                const uint32_t head = FILL ? pk[0][i] : 0u, fc = FILL ? pk[kPf][i] : 0u;
                 do {
                     const bool act = t < hi;
                     const int src = act ? static_cast<int>(t - fb) : 0;
-                    const uint32_t gv = static_cast<uint32_t>(__shfl(static_cast<int>(g), src, 64));
+                    uint32_t gv = static_cast<uint32_t>(__shfl(static_cast<int>(g), src, 64));
                     const uint32_t fv = static_cast<uint32_t>(__shfl(static_cast<int>(gflag), src, 64));
+                    if constexpr (FILL) {  // the head fragment: its raw sum without the field, folded here
+                        const uint32_t wv = static_cast<uint32_t>(__shfl(static_cast<int>(w), src, 64)) - fc;
+                        const uint32_t x = fold16(wv);
+                        gv = t != head ? gv : (fv & 1u) ? wv : (fv & 4u) ? x : (((x & 0xff) << 8) | (x >> 8));
+                    }
                     if (act) {
                         const uint32_t bad = (acc & kBad) | ((fv & 2u) ? kBad : 0u);
                         uint32_t s = (acc & 0xffffu) + gv;  // big: util.rs:89-99 mod 2^32; else <= 0x1fffe
@@ -1833,13 +1877,26 @@ __global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(
         }
         wave_lds_fence();
         for (uint32_t q = 0; q < K; ++q) {
-            const uint64_t p = base + q * 64 + lane;
+            const uint64_t p = static_cast<uint64_t>(base) + q * 64 + lane;
             const uint32_t acc = pk[2][q * 64 + lane];
             uint32_t r = acc & 0xffffu;
             if (a.flags & RNS_FLAG_COMPLEMENT)
                 r ^= 0xffff;
             const bool ok = !(acc & kBad);
-            if (p < a.n)
+            if constexpr (FILL) {
+                if (p < a.n && ok) {  // set_be16(&mut header[fo..fo + 2], result), header = fragment f0
+                    const uint32_t fo = a.field ? static_cast<uint32_t>(a.field[p]) : a.field_off;
+                    const uint64_t fp = a.off[pk[0][q * 64 + lane]] + a.base_adjust + fo;
+                    uint8_t *w8 = const_cast<uint8_t *>(a.arena);
+                    if (fp & 1) {
+                        w8[fp] = static_cast<uint8_t>(r >> 8);
+                        w8[fp + 1] = static_cast<uint8_t>(r);
+                    } else {
+                        *reinterpret_cast<uint16_t *>(w8 + fp) = static_cast<uint16_t>(((r & 0xff) << 8) | (r >> 8));
+                    }
+                }
+            }
+            if (p < a.n && (!FILL || a.out))
                 a.out[p] = static_cast<uint16_t>(ok ? r : 0u);  // 64 consecutive u16: one 128-byte store
             if (a.bad) {
                 const uint64_t rejected = __ballot(p < a.n && !ok);
@@ -2374,7 +2431,7 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : FILL ? RNS_ROWS_FILL_OCC : 8) voi
     uint32_t fo = 0;
     if constexpr (FILL)
         fo = a.field ? static_cast<uint32_t>(a.field[q]) : a.field_off;
-    const bool fok = FILL && live && ok && fo + 2u <= len;
+    const bool fok = FILL && live && ok && fo <= len && len - fo >= 2u;  // (no u32 wrap for any field_off)
     const uint64_t fpos = start + fo, fch = fpos & ~15ull;
     const uint32_t back = ((static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a.arena) >> 4) +
                             static_cast<uint32_t>(fch >> 4)) & (FC - 1u)) * 16u;

@@ -74,8 +74,11 @@ extern template int dispatch<true>(const CsumArgs &, uint32_t, uint32_t, uint32_
 int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st);
 int launch_fill_packed(const CsumArgs &a, hipStream_t st);
 int launch_stream_rx(const CsumArgs &a, hipStream_t st);
-// k_chain.hip: K packets per lane (1..kChainMaxK)
+// k_chain.hip: K packets per lane (1..kChainMaxK); FILL = the head-fragment fill
+template <bool FILL>
 int launch_chain(const CsumArgs &a, uint32_t K, bool nt, bool runs, hipStream_t st);
+extern template int launch_chain<false>(const CsumArgs &, uint32_t, bool, bool, hipStream_t);
+extern template int launch_chain<true>(const CsumArgs &, uint32_t, bool, bool, hipStream_t);
 // k_stash.hip: the class kernel's stash modes on one-wave workgroups
 int launch_fill(const CsumArgs &a, dim3 grid, hipStream_t st);
 int launch_rx(const CsumArgs &a, dim3 grid, hipStream_t st);

@@ -1,0 +1,389 @@
+"""Parity past 4 GiB: every product kernel instantiation that serves arenas of 4 GiB or
+more (the BUF=false forms: 64-bit global loads instead of buffer loads with 32-bit
+offsets) against the oracle.
+
+One 4 GiB + 64 MiB device arena.  Every batch lives in three windows of it: one near
+the start, one straddling the 4 GiB line, one ending at the arena's last byte.  The
+oracle runs over a host "mini arena" (the three windows back to back, descriptors
+translated), and for the in-place fills every byte of every window is compared.
+
+Entries covered: the packed checksum (rows kernel D = 8 and D = 16, the tiny rounds
+kernel, the unaligned-packing class kernel, a first block at an odd offset), the strided
+form, the packed and explicit transmit fills, packed and explicit receive verify, the
+transmit finalize, fragment chains (nontemporal and temporal class passes; the runs hint,
+which is ignored past 4 GiB) and the head-fragment chain fill.  Reference: util.rs:88-119,
+tcp.rs:838-850 / 957-973, udp.rs:158-171, icmp.rs:46-112, ip.rs:76-80 / 158-159.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from rustnetworkstack_amd import _lib
+from rustnetworkstack_amd.batch import (csum_batch_packed, csum_batch_strided, csum_chain, csum_fill,
+                                        csum_fill_packed, fill_splitmix64, packed_layout, rx_verify, rx_verify_packed,
+                                        tx_fill)
+from test_gpu_rx import make_packets
+from test_gpu_tx import outgoing
+from test_rx_oracle import L4, L6, ipv4, tcp_seg, R4
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+NBYTES = (4 << 30) + (64 << 20)
+FOUR_G = 1 << 32
+SPAN = 4 << 20  # bytes per window
+
+
+def dev(a, view):
+    return torch.from_numpy(np.ascontiguousarray(a).view(view)).to(DEV)
+
+
+def host_u16(t):
+    torch.cuda.synchronize()
+    return t.view(torch.int16).cpu().numpy().view(np.uint16)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu_present():
+    if not torch.cuda.is_available() or _lib.load().rns_device_count() == 0:
+        pytest.fail("gpu tests need a GPU (the HIP path has no CPU fallback)")
+
+
+class Windows:
+    """Three windows of the big arena: near its start, across the 4 GiB line, at its end."""
+
+    def __init__(self, arena):
+        self.arena = arena
+        self.starts = [4096, FOUR_G - SPAN // 2, NBYTES - SPAN]
+        self.orig = self.snapshot()
+
+    def snapshot(self):
+        torch.cuda.synchronize()
+        return [self.arena[s:s + SPAN].cpu().numpy() for s in self.starts]
+
+    def write(self, host_windows):
+        for s, h in zip(self.starts, host_windows):
+            self.arena[s:s + SPAN].copy_(torch.from_numpy(np.ascontiguousarray(h)))
+        torch.cuda.synchronize()
+
+    def restore(self):
+        self.write(self.orig)
+
+    def to_mini(self, k, off):
+        return np.asarray(off, dtype=np.uint64) - np.uint64(self.starts[k]) + np.uint64(k * SPAN)
+
+
+@pytest.fixture(scope="module")
+def win():
+    arena = torch.empty(NBYTES, dtype=torch.uint8, device=DEV)
+    fill_splitmix64(arena, 0xB16A)
+    w = Windows(arena)
+    assert arena.numel() >= FOUR_G  # the BUF=false instantiations
+    yield w
+    del w.arena, arena
+    torch.cuda.empty_cache()
+
+
+def packed_windows(win, lens_per_window, align_log2, shifts=(0, 0, 5)):
+    """Packed layouts, one per window (blocks of 64 packets never span windows: every window
+    but the last holds a multiple of 64 packets).  Returns device blk_off / len16, the
+    absolute and mini-arena offsets, lengths."""
+    blks, offs, minis, lens = [], [], [], []
+    for k, ln in enumerate(lens_per_window):
+        ln = np.asarray(ln, dtype=np.uint16)
+        assert k == len(lens_per_window) - 1 or ln.size % 64 == 0
+        blk, off, end = packed_layout(ln, align_log2, win.starts[k] + shifts[k])
+        assert end <= win.starts[k] + SPAN
+        blks.append(blk)
+        offs.append(off)
+        minis.append(win.to_mini(k, off))
+        lens.append(ln)
+    blk = np.concatenate(blks).astype(np.uint64)
+    return (dev(blk, np.int64), np.concatenate(offs), np.concatenate(minis), np.concatenate(lens))
+
+
+def imix_lengths(n, salt):
+    w = O.splitmix64_words(0x1A1A + salt, n)
+    return np.array([40, 40, 40, 40, 40, 40, 40, 576, 576, 576, 576, 1500], dtype=np.uint16)[w % np.uint64(12)]
+
+
+def lengths_for(kind, salt):
+    if kind == "imix":
+        return [imix_lengths(64 * 30, salt + k) for k in range(2)] + [imix_lengths(64 * 30 + 17, salt + 2)]
+    if kind == "mtu":
+        out = []
+        for k in range(3):
+            ln = np.full(64 * 20 + (7 if k == 2 else 0), 1500, dtype=np.uint16)
+            ln[3::17] = (O.splitmix64_words(salt + k, ln[3::17].size) % np.uint64(3000)).astype(np.uint16)
+            ln[5::29] = 0
+            out.append(ln)
+        return out
+    if kind == "tiny":
+        return [np.full(64 * 200, 64, dtype=np.uint16) for _ in range(2)] + [np.full(64 * 200 + 9, 64, np.uint16)]
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind,hint,align_log2", [
+    ("imix", 340, 4),    # rows kernel, D = 8, BUF=false
+    ("mtu", 1500, 4),    # rows kernel, D = 16, BUF=false
+    ("tiny", 64, 4),     # rounds kernel (tiny), BUF=false
+    ("imix", 340, 0),    # unaligned packing: class kernel, packed form, BUF=false
+    ("mtu", 1500, 1),    # the same, nontemporal
+])
+def test_packed_checksum(oracle, win, kind, hint, align_log2):
+    lens = lengths_for(kind, hint + align_log2)
+    blk, _, mini_off, ln = packed_windows(win, lens, align_log2)
+    seeds = (O.splitmix64_words(0x5EED + hint, ln.size) & np.uint64(0xFFFF)).astype(np.uint16)
+    mini = np.concatenate(win.orig)
+    want = oracle.batch(mini, mini_off, ln.astype(np.uint32), seeds, complement=True)
+    bad = torch.zeros(1, dtype=torch.int32, device=DEV)
+    got = host_u16(csum_batch_packed(win.arena, blk, dev(ln, np.int16), dev(seeds, np.int16), align_log2=align_log2,
+                                     complement=True, len_hint=hint, bad=bad))
+    diff = np.flatnonzero(got != want)
+    assert diff.size == 0, [(int(i), int(got[i]), int(want[i])) for i in diff[:5]]
+    assert int(bad.item()) == 0
+
+
+def test_strided_across_the_line(oracle, win):
+    n, stride, L = 20_000, 80, 64
+    first = FOUR_G - 64 * 10_000 - 3
+    want_arena = win.arena[first:first + n * stride].cpu().numpy()
+    off = np.arange(n, dtype=np.uint64) * np.uint64(stride)
+    want = oracle.batch(want_arena, off, np.full(n, L, dtype=np.uint32), None, complement=True)
+    got = host_u16(csum_batch_strided(win.arena, n, stride, L, first_off=first, complement=True))
+    assert np.array_equal(got, want)
+
+
+def expected_fill(oracle, mini, mini_off, ln, seeds, field):
+    """Zero each field that fits (alloc_header), 0xffff ^ ones_comp(seed, packet), the result
+    stored big-endian; a packet too short for its field yields 0 and is untouched."""
+    a = mini.copy()
+    fits = field.astype(np.int64) + 2 <= ln.astype(np.int64)
+    idx = mini_off.astype(np.int64) + field.astype(np.int64)
+    a[idx[fits]] = 0
+    a[idx[fits] + 1] = 0
+    want = oracle.batch(a, mini_off, ln.astype(np.uint32), seeds, complement=True)
+    want[~fits] = 0
+    a[idx[fits]] = (want[fits] >> 8).astype(np.uint8)
+    a[idx[fits] + 1] = (want[fits] & 0xFF).astype(np.uint8)
+    return want, fits, a
+
+
+@pytest.mark.parametrize("kind,hint", [("imix", 340), ("mtu", 1500)])
+def test_packed_fill(oracle, win, kind, hint):
+    lens = lengths_for(kind, 77 + hint)
+    blk, _, mini_off, ln = packed_windows(win, lens, 4, shifts=(0, 16, 32))
+    n = ln.size
+    seeds = (O.splitmix64_words(0xF1 + hint, n) & np.uint64(0xFFFF)).astype(np.uint16)
+    field = np.array([16, 6, 2, 10, 3, 17, 15, 31], dtype=np.uint16)[O.splitmix64_words(0xF2, n) % np.uint64(8)]
+    mini = np.concatenate(win.orig)
+    want, fits, want_arena = expected_fill(oracle, mini, mini_off, ln, seeds, field)
+    out = torch.empty(n, dtype=torch.uint16, device=DEV)
+    bad = torch.zeros(1, dtype=torch.int32, device=DEV)
+    try:
+        csum_fill_packed(win.arena, blk, dev(ln, np.int16), dev(seeds, np.int16), field=dev(field, np.int16), out=out,
+                         len_hint=hint, bad=bad)
+        assert np.array_equal(host_u16(out), want)
+        assert int(bad.item()) == int((~fits).sum())
+        got = np.concatenate(win.snapshot())
+        diff = np.flatnonzero(got != want_arena)
+        assert diff.size == 0, [(int(d), int(got[d]), int(want_arena[d])) for d in diff[:8]]
+    finally:
+        win.restore()
+
+
+def explicit_windows(win, per_window, salt, max_len=1600, min_gap=0):
+    """Packets at arbitrary offsets (any alignment) in every window."""
+    offs, minis, lens = [], [], []
+    for k in range(3):
+        w = O.splitmix64_words(0xE0 + salt + k, 2 * per_window)
+        ln = (w[:per_window] % np.uint64(max_len)).astype(np.int64)
+        gap = (w[per_window:] % np.uint64(23)).astype(np.int64) + min_gap
+        pos = np.cumsum(gap + np.concatenate([[0], ln[:-1]])) + 7 * k
+        assert pos[-1] + ln[-1] <= SPAN
+        off = (pos + win.starts[k]).astype(np.uint64)
+        offs.append(off)
+        minis.append(win.to_mini(k, off))
+        lens.append(ln.astype(np.uint32))
+    return np.concatenate(offs), np.concatenate(minis), np.concatenate(lens)
+
+
+def test_explicit_fill(oracle, win):
+    off, mini_off, ln = explicit_windows(win, 2000, 1)
+    n = ln.size
+    seeds = (O.splitmix64_words(0xF3, n) & np.uint64(0xFFFF)).astype(np.uint16)
+    field = np.array([16, 6, 2, 10, 3, 17], dtype=np.uint16)[O.splitmix64_words(0xF4, n) % np.uint64(6)]
+    mini = np.concatenate(win.orig)
+    want, fits, want_arena = expected_fill(oracle, mini, mini_off, ln, seeds, field)
+    out = torch.empty(n, dtype=torch.uint16, device=DEV)
+    bad = torch.zeros(1, dtype=torch.int32, device=DEV)
+    try:
+        csum_fill(win.arena, dev(off, np.int64), dev(ln, np.int32), dev(seeds, np.int16), field=dev(field, np.int16),
+                  out=out, bad=bad)
+        assert np.array_equal(host_u16(out), want)
+        assert int(bad.item()) == int((~fits).sum())
+        got = np.concatenate(win.snapshot())
+        diff = np.flatnonzero(got != want_arena)
+        assert diff.size == 0, [(int(d), int(got[d]), int(want_arena[d])) for d in diff[:8]]
+    finally:
+        win.restore()
+
+
+def place(win, pkts_per_window, offs_per_window):
+    """Write datagrams into the windows (device and the host copies)."""
+    host = [h.copy() for h in win.orig]
+    for k, (pk, off) in enumerate(zip(pkts_per_window, offs_per_window)):
+        for o, p in zip(off, pk):
+            r = int(o) - win.starts[k]
+            host[k][r:r + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    win.write(host)
+    return host
+
+
+def datagrams(seed):
+    """Per window: 128 ACK-sized TCP/IPv4 datagrams (a unit that skips the rows) then a mix
+    of every kind the receive path distinguishes."""
+    out = []
+    for k in range(3):
+        acks = [ipv4(6, tcp_seg(R4, L4, bytes([k, i]) * (i % 3))) for i in range(128)]
+        out.append(acks + make_packets(640 + (11 if k == 2 else 0), seed + k))
+    return out
+
+
+def test_packed_receive_verify(oracle, win):
+    pk = datagrams(0x9A)
+    lens = [np.array([len(p) for p in w], dtype=np.uint16) for w in pk]
+    blk, off, _, ln = packed_windows(win, lens, 4, shifts=(0, 0, 0))
+    cuts = np.cumsum([0] + [len(w) for w in pk])
+    try:
+        place(win, pk, [off[cuts[k]:cuts[k + 1]] for k in range(3)])
+        flat = [p for w in pk for p in w]
+        want = [O.rx_verify_ref(p, L4, L6, ones_comp=oracle.compute_ones_comp) for p in flat]
+        l4 = torch.empty(len(flat), dtype=torch.uint16, device=DEV)
+        st = rx_verify_packed(win.arena, blk, dev(ln, np.int16), L4, L6, l4_sum=l4)
+        torch.cuda.synchronize()
+        got = st.cpu().numpy()
+        want_st = np.array([w[0] for w in want], dtype=np.uint8)
+        assert len(set(want_st.tolist())) >= 5
+        diff = np.flatnonzero(got != want_st)
+        assert diff.size == 0, [(int(i), int(got[i]), int(want_st[i])) for i in diff[:5]]
+        assert np.array_equal(host_u16(l4), np.array([w[1] for w in want], dtype=np.uint16))
+    finally:
+        win.restore()
+
+
+def test_explicit_receive_verify(oracle, win):
+    pk = datagrams(0x9B)
+    offs = []
+    for k, w in enumerate(pk):
+        g = O.splitmix64_words(0x77 + k, len(w)) % np.uint64(16)
+        pos = np.cumsum(np.array([len(p) for p in w], dtype=np.int64) + g.astype(np.int64)) - \
+            np.array([len(p) for p in w], dtype=np.int64) + 3 * k
+        offs.append((pos + win.starts[k]).astype(np.uint64))
+    try:
+        place(win, pk, offs)
+        flat = [p for w in pk for p in w]
+        off = np.concatenate(offs)
+        ln = np.array([len(p) for p in flat], dtype=np.uint32)
+        want = [O.rx_verify_ref(p, L4, L6, ones_comp=oracle.compute_ones_comp) for p in flat]
+        l4 = torch.empty(len(flat), dtype=torch.uint16, device=DEV)
+        st = rx_verify(win.arena, dev(off, np.int64), dev(ln, np.int32), L4, L6, l4_sum=l4)
+        torch.cuda.synchronize()
+        assert np.array_equal(st.cpu().numpy(), np.array([w[0] for w in want], dtype=np.uint8))
+        assert np.array_equal(host_u16(l4), np.array([w[1] for w in want], dtype=np.uint16))
+    finally:
+        win.restore()
+
+
+def test_transmit_finalize(oracle, win):
+    pk = [outgoing(700, 0x7A + k) for k in range(3)]
+    offs = []
+    for k, w in enumerate(pk):
+        g = O.splitmix64_words(0x78 + k, len(w)) % np.uint64(16)
+        ln = np.array([len(p) for p in w], dtype=np.int64)
+        pos = np.cumsum(ln + g.astype(np.int64)) - ln + 5 * k
+        offs.append((pos + win.starts[k]).astype(np.uint64))
+    try:
+        host = place(win, pk, offs)
+        want_st = []
+        for k, (w, off) in enumerate(zip(pk, offs)):
+            for o, p in zip(off, w):
+                q, s = O.tx_fill_ref(p, ones_comp=oracle.compute_ones_comp)
+                r = int(o) - win.starts[k]
+                host[k][r:r + len(q)] = np.frombuffer(q, dtype=np.uint8)
+                want_st.append(s)
+        flat = [p for w in pk for p in w]
+        off = np.concatenate(offs)
+        ln = np.array([len(p) for p in flat], dtype=np.uint32)
+        st = tx_fill(win.arena, dev(off, np.int64), dev(ln, np.int32))
+        torch.cuda.synchronize()
+        assert np.array_equal(st.cpu().numpy(), np.array(want_st, dtype=np.uint8))
+        got = np.concatenate(win.snapshot())
+        want = np.concatenate(host)
+        diff = np.flatnonzero(got != want)
+        assert diff.size == 0, [(int(d), int(got[d]), int(want[d])) for d in diff[:8]]
+    finally:
+        win.restore()
+
+
+def chain_windows(win, per_window, salt, max_frag):
+    """Chains of 1-6 fragments scattered over every window (any alignment, odd sizes)."""
+    offs, minis, lens, first = [], [], [], [0]
+    for k in range(3):
+        w = O.splitmix64_words(0xC0 + salt + k, 3 * per_window)
+        nfr = (w[:per_window] % np.uint64(6)).astype(np.int64) + 1
+        tot = int(nfr.sum())
+        fl = (O.splitmix64_words(0xC8 + salt + k, tot) % np.uint64(max_frag)).astype(np.int64) + 1
+        gap = (O.splitmix64_words(0xC9 + salt + k, tot) % np.uint64(40)).astype(np.int64)
+        pos = np.cumsum(fl + gap) - fl + 9 * k
+        assert pos[-1] + fl[-1] <= SPAN
+        perm = np.argsort(O.splitmix64_words(0xCA + salt + k, tot))  # scatter the fragments
+        off = (pos[perm] + win.starts[k]).astype(np.uint64)
+        offs.append(off)
+        minis.append(win.to_mini(k, off))
+        lens.append(fl[perm].astype(np.uint32))
+        for c in nfr:
+            first.append(first[-1] + int(c))
+    return np.concatenate(offs), np.concatenate(minis), np.concatenate(lens), np.array(first, dtype=np.uint32)
+
+
+@pytest.mark.parametrize("hint,runs", [(512, False), (100, False), (512, True)])
+def test_chains(oracle, win, hint, runs):
+    off, mini_off, ln, first = chain_windows(win, 1500, hint, 2 * hint)
+    n = first.size - 1
+    seeds = (O.splitmix64_words(0xCB + hint, n) & np.uint64(0xFFFF)).astype(np.uint16)
+    mini = np.concatenate(win.orig)
+    want = oracle.chain_batch(mini, mini_off, ln, first, seeds, complement=True)
+    got = host_u16(csum_chain(win.arena, dev(off, np.int64), dev(ln, np.int32), dev(first, np.int32),
+                              dev(seeds, np.int16), complement=True, frag_len_hint=hint, runs=runs))
+    diff = np.flatnonzero(got != want)
+    assert diff.size == 0, [(int(i), int(got[i]), int(want[i])) for i in diff[:5]]
+
+
+def test_chain_fill(oracle, win):
+    """Head-fragment fill (rns_csum_chain_fill_dev): the chain folded like util.rs:112-119
+    with the field counted as zero, stored big-endian into the head fragment."""
+    from rustnetworkstack_amd.batch import csum_chain_fill
+    off, mini_off, ln, first = chain_windows(win, 1500, 7, 600)
+    n = first.size - 1
+    ln[first[:-1]] = np.maximum(ln[first[:-1]], 20)      # head fragments hold a 20-byte header
+    seeds = (O.splitmix64_words(0xCC, n) & np.uint64(0xFFFF)).astype(np.uint16)
+    field = np.array([16, 6, 2, 10], dtype=np.uint16)[np.arange(n) % 4]
+    mini = np.concatenate(win.orig)
+    want_arena = mini.copy()
+    heads = mini_off[first[:-1]].astype(np.int64) + field.astype(np.int64)
+    want_arena[heads] = 0
+    want_arena[heads + 1] = 0
+    want = oracle.chain_batch(want_arena, mini_off, ln, first, seeds, complement=True)
+    want_arena[heads] = (want >> 8).astype(np.uint8)
+    want_arena[heads + 1] = (want & 0xFF).astype(np.uint8)
+    out = torch.empty(n, dtype=torch.uint16, device=DEV)
+    try:
+        csum_chain_fill(win.arena, dev(off, np.int64), dev(ln, np.int32), dev(first, np.int32), dev(seeds, np.int16),
+                        field=dev(field, np.int16), out=out, frag_len_hint=512)
+        assert np.array_equal(host_u16(out), want)
+        got = np.concatenate(win.snapshot())
+        diff = np.flatnonzero(got != want_arena)
+        assert diff.size == 0, [(int(d), int(got[d]), int(want_arena[d])) for d in diff[:8]]
+    finally:
+        win.restore()

@@ -129,6 +129,33 @@ def test_tiny_packets(oracle):
     check_fill(oracle, np.full(n, 64), np.full(n, 16), len_hint=64, field_arg=False)
 
 
+@pytest.mark.parametrize("field_off", [0xFFFFFFFF, 0xFFFFFFFE, 0x10000, 65534])
+def test_field_offset_past_every_packet(field_off):
+    """A field offset no packet can hold (the u32 sum fo + 2 would wrap for the first two):
+    through the bare C ABI every packet is rejected and counted, and no arena byte changes."""
+    n = 64 * 3 + 5
+    ln = np.full(n, 1500, dtype=np.uint16)
+    ln[::7] = 65535
+    blk, off, end = packed_layout(ln, 4, 0)
+    arena_np = O.splitmix64_bytes(0xF0F0, end + 64)
+    arena = torch.from_numpy(arena_np.copy()).to(DEV)
+    d_blk, d_len = dev(blk.astype(np.uint64), np.int64), dev(ln, np.int16)
+    out = torch.full((n,), 0x1234, dtype=torch.int16, device=DEV)
+    bad = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for hint in (340, 1500):
+        bad.zero_()
+        st = _lib.load().rns_csum_fill_packed_dev(arena.data_ptr(), arena.numel(), d_blk.data_ptr(), d_len.data_ptr(),
+                                                  4, None, None, field_off, out.data_ptr(), n,
+                                                  _lib.RNS_FLAG_COMPLEMENT, hint, bad.data_ptr(), None)
+        assert st == _lib.RNS_OK
+        torch.cuda.synchronize()
+        assert int(bad.item()) == n
+        assert (host_u16(out) == 0).all()
+        assert np.array_equal(arena.cpu().numpy(), arena_np)
+    with pytest.raises(ValueError):
+        csum_fill_packed(arena, d_blk, d_len, field_off=min(field_off, 1 << 31))
+
+
 def test_misaligned_packing_is_invalid():
     arena = torch.zeros(256, dtype=torch.uint8, device=DEV)
     with pytest.raises(ValueError):
