@@ -321,6 +321,57 @@ class BadCountReduce:
         return self.total
 
 
+class OverlappedGather:
+    """The §8(e) all-gather of step i's results overlapped with step i+1's compute:
+    the kernel of step i goes to the launch stream, its all-gather to a side stream that waits
+    only for that kernel; the next step's kernel (an independent batch) starts at once.  Before
+    a kernel rewrites a batch's results it waits for the gather that still reads them (batches
+    rotate, so with two or more batches one gather is always in flight under the next kernel).
+    Under gloo (CPU tests, host-staged) the gather is synchronous: the same steps, no overlap."""
+
+    def __init__(self, engine):
+        torch = engine.torch
+        self.engine, self.torch = engine, torch
+        dev = getattr(engine, "device", None)
+        self.side = torch.cuda.Stream(device=dev) if dev is not None and dev.type == "cuda" else None
+        self.pending = {}  # batch index -> event: its last gather has finished reading its results
+
+    def __call__(self):
+        eng, torch = self.engine, self.torch
+        i = eng.k % len(eng.batches)
+        if self.side is None:
+            eng.step()
+            eng.gather()
+            return
+        ev = self.pending.get(i)
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+        eng.step()
+        ready = torch.cuda.Event()
+        ready.record()
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(ready)
+            eng.gather()
+            done = torch.cuda.Event()
+            done.record(self.side)
+        self.pending[i] = done
+
+
+def rank_parity(engine, threads: int = 8) -> dict:
+    """This rank's own check of the GPU results: every packet of its first batch (the batch
+    the timed steps, and the gather legs after them, left results in) against the oracle's
+    restatement of util.rs:88-106, on the host.  Test infrastructure, after all timing."""
+    import numpy as np
+
+    from oracle.oracle import get_oracle
+    b = engine.batches[0]
+    lay = b.layout
+    arena = b.arena[:lay.arena_bytes].cpu().numpy()
+    want = get_oracle().batch(arena, lay.off, lay.length, lay.seed, complement=True, threads=threads, check=False)
+    got = b.out.view(engine.torch.int16).cpu().numpy().view(np.uint16)
+    return {"bit_exact": bool(np.array_equal(got[:lay.n], want)), "packets": int(lay.n)}
+
+
 # ---------------------------------------------------------------------------
 # GPU engine: the product path
 # ---------------------------------------------------------------------------
@@ -906,15 +957,47 @@ def main(argv=None):
     elif dist.world > 1 and not args.no_gather:
         # the same steps plus one all-gather of every rank's results, and the gather alone
         engine.gatherer = ResultGather(dist, engine.n, engine.device)
+        # every collective leg runs eagerly (one C-ABI call and one collective call per step); the
+        # compute-only leg is re-timed the same way so the two compare like for like
+        re_ = timed_loop(engine, dist, args.steps, args.warmup)
         rg = timed_loop(engine, dist, args.steps, args.warmup, step=engine.step_and_gather)
+        ro = timed_loop(engine, dist, args.steps, args.warmup, step=OverlappedGather(engine))
         rgo = timed_loop(engine, dist, args.steps, args.warmup, step=engine.gather)
         line["value_compute"] = line["value"]
+        line["value_compute_eager"] = round(total_bytes / re_["elapsed_s"] / 2 ** 30, 2)
         line["value_gather"] = round(total_bytes / rg["elapsed_s"] / 2 ** 30, 2)
         line["ms_per_step_gather"] = round(rg["elapsed_s"] * 1e3 / args.steps, 4)
+        line["value_gather_overlap"] = round(total_bytes / ro["elapsed_s"] / 2 ** 30, 2)
+        line["ms_per_step_gather_overlap"] = round(ro["elapsed_s"] * 1e3 / args.steps, 4)
         line["gather_ms"] = round(rgo["elapsed_s"] * 1e3 / args.steps, 4)
         line["gather"] = {"collective": f"all_gather_into_tensor ({dist.backend}) of uint8 results",
                           "bytes_per_rank": engine.gatherer.bytes_per_rank,
                           "bytes_received_per_rank": engine.gatherer.bytes_per_rank * (dist.world - 1)}
+        line["legs"] = {
+            "value / value_compute": "compute only; the K steps as one HIP graph replay (the N=1 timing)",
+            "value_compute_eager": "compute only; one C-ABI launch per step from the host (the gather legs' mode)",
+            "value_gather": "eager; each step's kernel, then its all-gather, in order on one stream",
+            "value_gather_overlap": "eager; step i's all-gather on a side stream under step i+1's kernel "
+                                    "(OverlappedGather, DESIGN §6)",
+            "gather_ms": "eager; the all-gather alone, per step"}
+    if dist.world > 1 and not verify:
+        # after every rank's GPU legs: each rank checks its own results; rank 0 times the CPU
+        # baseline on its own batch while the others wait (benches/util_bench.rs:20-45 beside
+        # the N-GPU figure, on the same box's host cores, in the same run)
+        par = rank_parity(engine, threads=max(1, min(8, cpu_grant()["threads"])))
+        ranks_exact = int(dist.sum(1.0 if par["bit_exact"] else 0.0))
+        checked = int(dist.sum(float(par["packets"])))
+        dist.barrier()
+        if dist.rank == 0 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(engine, args.cpu_seconds)
+            line["cpu_baseline"]["sample"] = "rank 0's batch: " + line["cpu_baseline"]["sample"]
+            line["cpu_baseline"]["gpu_sample_bit_exact_rank0"] = line["cpu_baseline"]["gpu_sample_bit_exact"]
+            line["cpu_baseline"]["gpu_sample_bit_exact"] = ranks_exact == dist.world
+        dist.barrier()
+        line["parity"] = {"ranks_bit_exact": ranks_exact, "ranks": dist.world, "packets_checked": checked,
+                          "bit_exact_all_ranks": ranks_exact == dist.world,
+                          "how": "every rank: every packet of its first batch vs the oracle (util.rs:88-106 "
+                                 "restated), after the timed legs; the counts are all-reduced"}
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(engine, args.cpu_seconds)
     if dist.rank == 0 and dist.world == 1 and not args.no_host_pipeline:

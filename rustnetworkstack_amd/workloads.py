@@ -282,3 +282,79 @@ def make_verify_batch(b: "DeviceBatch") -> None:
         b.arena[p] ^= 0x5A
     b.status = torch.empty(lay.n, dtype=torch.uint8, device=dev)
     b.expected_bad = int(sel.size)
+
+
+# ---------------------------------------------------------------------------
+# Transmit chains (rns_csum_chain_fill_dev): the shape tcp_output checksums
+# (tcp.rs:938-973).  alloc_header prepends a head fragment holding the TCP header
+# (buf.rs:262-291); the payload follows as the NetBuffer's data fragments.  A batching
+# transmit path keeps the head fragments of consecutive packets back to back in a
+# header region, so a wave's field stores share cache lines, and the payloads in a
+# payload region.
+# ---------------------------------------------------------------------------
+@dataclass
+class TxChainLayout:
+    """Fragment chains of a transmit batch: packet i = fragments first[i] .. first[i+1]
+    (the head fragment first), its checksum field at byte `field` of the head."""
+    name: str
+    frag_off: np.ndarray   # uint64
+    frag_len: np.ndarray   # uint32
+    first: np.ndarray      # uint32 [n + 1]
+    seed: np.ndarray       # uint16
+    field: int
+    head: int
+    arena_bytes: int
+    data_seed: int
+    payload_bytes: int     # sum of the packets' lengths (head + payload), the metric's bytes
+
+    @property
+    def n(self) -> int:
+        return int(self.first.shape[0] - 1)
+
+
+def tx_chain_layout(name: str, n: int | None = None, head: int = 20, frag: int = 0, field: int = 16,
+                    data_seed: int = DATA_SEED, shard: tuple[int, int] = (0, 1)) -> TxChainLayout:
+    """Packet i of config `name` (length L_i) as [a `head`-byte head fragment, L_i - head
+    payload bytes].  Heads lie back to back in packet order from offset 0 (a header region
+    of n * head bytes, padded to 4 KiB); payloads follow, 16-byte aligned and back to back,
+    as one fragment (frag = 0) or as fragments of `frag` bytes, the last shorter (NetBuffer
+    data fragments: frag = 512, buf.rs:50).  Seeds as make_layout's (the pseudo-header sums
+    the caller passes)."""
+    lay = make_layout(name, n=n, data_seed=data_seed, shard=shard)
+    L = lay.length.astype(np.int64)
+    h = np.minimum(L, head)
+    pay = L - h
+    nh = lay.n
+    hoff = np.zeros(nh, dtype=np.int64)
+    if nh > 1:
+        np.cumsum(h[:-1], out=hoff[1:])
+    base = (int(h.sum()) + 4095) & ~4095
+    padded = (pay + ALIGN - 1) & ~(ALIGN - 1)
+    poff = np.zeros(nh, dtype=np.int64)
+    if nh > 1:
+        np.cumsum(padded[:-1], out=poff[1:])
+    poff += base
+    if frag <= 0:
+        nfp = (pay > 0).astype(np.int64)
+    else:
+        nfp = (pay + frag - 1) // frag
+    nfr = 1 + nfp
+    first = np.zeros(nh + 1, dtype=np.int64)
+    np.cumsum(nfr, out=first[1:])
+    nf = int(first[-1])
+    off = np.zeros(nf, dtype=np.int64)
+    ln = np.zeros(nf, dtype=np.int64)
+    off[first[:-1]] = hoff
+    ln[first[:-1]] = h
+    pk = np.repeat(np.arange(nh), nfp)                 # packet of every payload fragment
+    is_pay = np.ones(nf, dtype=bool)
+    is_pay[first[:-1]] = False
+    pidx = np.flatnonzero(is_pay)                       # fragment indices of the payload fragments
+    k = pidx - first[pk] - 1                            # fragment number within the payload
+    step = frag if frag > 0 else 0
+    off[pidx] = poff[pk] + k * step
+    ln[pidx] = pay[pk] if step == 0 else np.minimum(pay[pk] - k * step, step)
+    arena_bytes = int(poff[-1] + padded[-1]) if nh else base
+    return TxChainLayout(name=name, frag_off=off.astype(np.uint64), frag_len=ln.astype(np.uint32),
+                         first=first.astype(np.uint32), seed=lay.seed, field=field, head=head,
+                         arena_bytes=arena_bytes, data_seed=lay.data_seed, payload_bytes=lay.payload_bytes)

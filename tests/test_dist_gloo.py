@@ -27,8 +27,9 @@ N = {n}
 ENGINES = []
 
 class _Batch:
-    def __init__(self, layout):
+    def __init__(self, layout, arena):
         self.layout = layout
+        self.arena = torch.from_numpy(arena)
         self.out = torch.zeros(layout.n, dtype=torch.uint16)
 
 class CpuEngine(bench.GpuEngine):
@@ -43,7 +44,7 @@ class CpuEngine(bench.GpuEngine):
         else:
             self.layout = make_layout(config, n=N, data_seed=0x5EEDC0DE + 0x1000 * rank)
         self.arena = splitmix64_bytes(self.layout.data_seed, self.layout.arena_bytes)
-        self.batches = [_Batch(self.layout)]
+        self.batches = [_Batch(self.layout, self.arena)]
         self.last = self.batches[0]
         self.compact, self.shape, self.k, self.timed = True, None, 0, 0
         self.packed, self.form = False, "32"
@@ -72,7 +73,7 @@ class CpuEngine(bench.GpuEngine):
 
 bench.GpuEngine = CpuEngine
 line = bench.main(["--gpus", "2", "--config", {config!r}, "--steps", "3", "--warmup", "1", "--median-launches", "3",
-                   "--traffic-json", "/nonexistent/{{config}}.json"])
+                   "--traffic-json", "/nonexistent/{{config}}.json", "--cpu-seconds", "0.5"])
 if line is None:   # the launching parent (bench.py --gpus 2 without torchrun): the ranks did the work
     sys.exit(0)
 eng = ENGINES[0]
@@ -124,9 +125,17 @@ def test_two_rank_gloo_bench_main(tmp_path, oracle, config, n, launch):
     strong = config == "c5_imix"
     assert line["scaling"] == ("strong" if strong else "weak")
     # the §8(e) legs: compute-only value, compute+gather, gather alone
-    for k in ("value_compute", "value_gather", "ms_per_step_gather", "gather_ms"):
+    for k in ("value_compute", "value_compute_eager", "value_gather", "ms_per_step_gather", "value_gather_overlap",
+              "ms_per_step_gather_overlap", "gather_ms"):
         assert k in line and line[k] > 0, k
     assert line["value_compute"] == line["value"]
+    assert set(line["legs"]) >= {"value_compute_eager", "value_gather", "value_gather_overlap", "gather_ms"}
+    # the CPU baseline beside the N-GPU figure (rank 0's batch) and every rank's own parity check
+    cb = line["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1 and cb["sample"].startswith("rank 0")
+    assert cb["gpu_sample_bit_exact"] is True and cb["gpu_sample_bit_exact_rank0"] is True
+    assert line["parity"]["bit_exact_all_ranks"] is True and line["parity"]["ranks_bit_exact"] == 2
+    assert line["parity"]["packets_checked"] == sum(res[r]["n"] for r in (0, 1))
     # aggregate bytes: strong = the shards add up to the one batch; weak = one full batch per rank
     whole = make_layout(config, n=n).payload_bytes
     per_rank = [res[r]["n"] for r in (0, 1)]

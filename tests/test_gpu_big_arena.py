@@ -20,9 +20,9 @@ import torch
 
 from oracle import oracle as O
 from rustnetworkstack_amd import _lib
-from rustnetworkstack_amd.batch import (csum_batch_packed, csum_batch_strided, csum_chain, csum_fill,
-                                        csum_fill_packed, fill_splitmix64, packed_layout, rx_verify, rx_verify_packed,
-                                        tx_fill)
+from rustnetworkstack_amd.batch import (csum_batch_packed, csum_batch_strided, csum_chain, csum_chain_fill,
+                                        csum_fill, csum_fill_packed, fill_splitmix64, packed_layout, rx_verify,
+                                        rx_verify_packed, tx_fill)
 from test_gpu_rx import make_packets
 from test_gpu_tx import outgoing
 from test_rx_oracle import L4, L6, ipv4, tcp_seg, R4
@@ -326,22 +326,27 @@ def test_transmit_finalize(oracle, win):
         win.restore()
 
 
-def chain_windows(win, per_window, salt, max_frag):
-    """Chains of 1-6 fragments scattered over every window (any alignment, odd sizes)."""
+def chain_windows(win, per_window, salt, max_frag, min_head=1):
+    """Chains of 1-6 fragments scattered over every window (any alignment, odd sizes); a
+    packet's first fragment has at least min_head bytes."""
     offs, minis, lens, first = [], [], [], [0]
     for k in range(3):
         w = O.splitmix64_words(0xC0 + salt + k, 3 * per_window)
         nfr = (w[:per_window] % np.uint64(6)).astype(np.int64) + 1
         tot = int(nfr.sum())
+        heads = np.concatenate([[0], np.cumsum(nfr[:-1])])
         fl = (O.splitmix64_words(0xC8 + salt + k, tot) % np.uint64(max_frag)).astype(np.int64) + 1
+        fl[heads] = np.maximum(fl[heads], min_head)
         gap = (O.splitmix64_words(0xC9 + salt + k, tot) % np.uint64(40)).astype(np.int64)
-        pos = np.cumsum(fl + gap) - fl + 9 * k
-        assert pos[-1] + fl[-1] <= SPAN
-        perm = np.argsort(O.splitmix64_words(0xCA + salt + k, tot))  # scatter the fragments
-        off = (pos[perm] + win.starts[k]).astype(np.uint64)
+        order = np.argsort(O.splitmix64_words(0xCA + salt + k, tot))  # memory order: scattered fragments
+        pos = np.cumsum(fl[order] + gap) - fl[order] + 9 * k
+        assert pos[-1] + fl[order][-1] <= SPAN
+        at = np.empty(tot, dtype=np.int64)
+        at[order] = pos
+        off = (at + win.starts[k]).astype(np.uint64)
         offs.append(off)
         minis.append(win.to_mini(k, off))
-        lens.append(fl[perm].astype(np.uint32))
+        lens.append(fl.astype(np.uint32))
         for c in nfr:
             first.append(first[-1] + int(c))
     return np.concatenate(offs), np.concatenate(minis), np.concatenate(lens), np.array(first, dtype=np.uint32)
@@ -363,10 +368,8 @@ def test_chains(oracle, win, hint, runs):
 def test_chain_fill(oracle, win):
     """Head-fragment fill (rns_csum_chain_fill_dev): the chain folded like util.rs:112-119
     with the field counted as zero, stored big-endian into the head fragment."""
-    from rustnetworkstack_amd.batch import csum_chain_fill
-    off, mini_off, ln, first = chain_windows(win, 1500, 7, 600)
+    off, mini_off, ln, first = chain_windows(win, 1500, 7, 600, min_head=20)  # heads hold a 20-byte header
     n = first.size - 1
-    ln[first[:-1]] = np.maximum(ln[first[:-1]], 20)      # head fragments hold a 20-byte header
     seeds = (O.splitmix64_words(0xCC, n) & np.uint64(0xFFFF)).astype(np.uint16)
     field = np.array([16, 6, 2, 10], dtype=np.uint16)[np.arange(n) % 4]
     mini = np.concatenate(win.orig)

@@ -9,6 +9,10 @@ batch checksum, on the headline batch (2^20 x 1500 B) and on IMIX:
 * verify   — rns_rx_verify_dev: IPv4 header + TCP checks of whole datagrams
 * tx       — rns_tx_fill_dev: IPv4 header + TCP checksums of whole datagrams stored in
              place, pseudo-headers formed on the device
+* chain_fill — rns_csum_chain_fill_dev on the transmit shape (workloads.tx_chain_layout:
+             20-byte TCP head fragments back to back in a header region, the payload as one
+             fragment or as 512-byte NetBuffer fragments), next to the plain chain checksum
+             of the same chains (chain_tx)
 
 Timing: one pair of HIP events around K back-to-back launches on the launch stream,
 median of R rounds.  GB/s counts algorithmic bytes (payload read + result bytes
@@ -106,6 +110,9 @@ def main():
                 for runs in (False, True):  # without / with RNS_FLAG_CHAIN_RUNS
                     r[key + ("_runs" if runs else "")] = bench_chain(b, lay, dev, args, runs) if cl == "packed" else \
                         bench_chain_netbuf(lay, dev, args, shuffled=cl == "netbuf_shuffled", runs=runs)
+        if "chain_fill" in ops:
+            for frag in (0, 512):
+                r.update(bench_chain_fill(cfg, dev, args, frag))
         if "fill" in ops:
             ms = timed(lambda: csum_fill(b.arena, b.off, b.length, b.seed, field_off=16), args.steps, args.rounds)
             r["fill"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1)}
@@ -175,6 +182,36 @@ def bench_chain(b, lay, dev, args, runs=False):
                                   frag_sums=sums, frag_len_hint=int(round(pay / nf)), runs=runs),
                args.steps, args.rounds)
     return {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1), "fragments": nf}
+
+
+def bench_chain_fill(cfg, dev, args, frag):
+    """The head-fragment fill and the plain chain checksum over the transmit shape."""
+    from rustnetworkstack_amd.batch import csum_chain_fill, fill_splitmix64
+    from rustnetworkstack_amd.workloads import tx_chain_layout
+    t = tx_chain_layout(cfg, frag=frag)
+    n, pay, nf = t.n, t.payload_bytes, int(t.frag_off.shape[0])
+    arena = torch.empty(t.arena_bytes + 64, dtype=torch.uint8, device=dev)
+    fill_splitmix64(arena, t.data_seed)
+    d_fo = torch.from_numpy(t.frag_off.view(np.int64)).to(dev)
+    d_fl = torch.from_numpy(t.frag_len.view(np.int32)).to(dev)
+    d_first = torch.from_numpy(t.first.view(np.int32)).to(dev)
+    seed = torch.from_numpy(t.seed.view(np.int16)).to(dev)
+    out = torch.empty(n, dtype=torch.uint16, device=dev)
+    hint = int(round(pay / nf))
+    tag = "tx" if frag == 0 else f"tx{frag}"
+    res = {}
+    for runs in (False, True):
+        sfx = "_runs" if runs else ""
+        ms = timed(lambda: csum_chain_fill(arena, d_fo, d_fl, d_first, seed, field_off=t.field, out=out,
+                                           frag_len_hint=hint, runs=runs), args.steps, args.rounds)
+        res[f"chain_fill_{tag}{sfx}"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1),
+                                        "fragments": nf, "hint": hint}
+        ms = timed(lambda: csum_chain(arena, d_fo, d_fl, d_first, seed, complement=True, out=out,
+                                      frag_len_hint=hint, runs=runs), args.steps, args.rounds)
+        res[f"chain_{tag}{sfx}"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1)}
+    del arena
+    torch.cuda.empty_cache()
+    return res
 
 
 def bench_chain_netbuf(lay, dev, args, shuffled=False, runs=False):
