@@ -55,6 +55,7 @@ extern "C" {
 /* ---- flags for batch calls ---------------------------------------------- */
 #define RNS_FLAG_COMPLEMENT 0x1u   /* store 0xffff ^ sum (the transmitted / verified value) */
 #define RNS_FLAG_CHAIN_RUNS 0x2u   /* rns_csum_chain_dev: fragments are often views of one buffer (see there) */
+#define RNS_FLAG_CHAIN_TX_PACKED 0x4u  /* chains: transmit-shaped, payloads packed (rns_csum_chain_fill_dev) */
 
 /* Fragment of a packet, same layout as the reference's `#[repr(C)] struct IOVec
  * { base: *const u8, len: usize }` (netif.rs:24-29). */
@@ -186,7 +187,15 @@ int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
  * must not overlap a field.  RNS_FLAG_CHAIN_RUNS: the hint of rns_csum_chain_dev (the
  * head fragment then starts each run).  Lay the head fragments of consecutive packets
  * back to back in a header region (a batching transmit path's header arena): a wave's
- * 64 field stores then land in a few cache lines instead of 64 scattered ones. */
+ * 64 field stores then land in a few cache lines instead of 64 scattered ones.
+ * RNS_FLAG_CHAIN_TX_PACKED (a hint for this entry and rns_csum_chain_dev; results are
+ * identical without it): packets are [a head fragment with (start & 15) + length <= 64,
+ * then payload fragments (at most 4) that form a run: back to back, even non-final
+ * lengths, <= 65535 bytes], and the payloads of consecutive packets ascend at 16-byte-
+ * aligned starts (a packed payload region).  Each 64-packet block's payloads then stream
+ * as one region (the rows kernel) while every owner sums its own head; a block that does
+ * not have this shape takes an exact per-packet loop (slow; use the hint only for such
+ * batches). */
 int rns_csum_chain_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_frag_off,
                             const uint32_t *d_frag_len, uint32_t n_frags, const uint32_t *d_first,
                             const uint16_t *d_seed, const uint16_t *d_field, uint32_t field_off, uint16_t *d_out,

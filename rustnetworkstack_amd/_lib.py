@@ -25,6 +25,7 @@ RNS_E_IO = -7
 RNS_E_HIP_BASE = -1000
 RNS_FLAG_COMPLEMENT = 0x1
 RNS_FLAG_CHAIN_RUNS = 0x2
+RNS_FLAG_CHAIN_TX_PACKED = 0x4
 RNS_RX_IP_OK = 0x01
 RNS_RX_L4_OK = 0x02
 RNS_RX_L4_UNCHECKED = 0x04

@@ -309,14 +309,15 @@ def csum_batch_strided(arena: torch.Tensor, n: int, stride: int, length: int, *,
 def csum_chain(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch.Tensor, first: torch.Tensor,
                seed: torch.Tensor | None = None, *, complement: bool = False, out: torch.Tensor | None = None,
                frag_sums: torch.Tensor | None = None, bad: torch.Tensor | None = None,
-               frag_len_hint: int = 512, runs: bool = False) -> torch.Tensor:
+               frag_len_hint: int = 512, runs: bool = False, tx_packed: bool = False) -> torch.Tensor:
     """util.rs:112 ``compute_buffer_ones_comp`` for a batch of fragment chains.
 
     Packet i = fragments ``first[i] .. first[i+1]`` (``first``: int32 [n+1]) of
     ``(frag_off, frag_len)``; each fragment is folded on its own like the reference,
     in one pass (``frag_sums`` is accepted for compatibility and unused).
     ``runs``: RNS_FLAG_CHAIN_RUNS, the hint that fragments are often back-to-back
-    views of one buffer (same results either way).
+    views of one buffer (same results either way).  ``tx_packed``: RNS_FLAG_CHAIN_TX_PACKED
+    (see csum_chain_fill).
     """
     _require_cuda(arena, "arena", (torch.uint8,))
     _require_cuda(frag_off, "frag_off", (torch.int64,))
@@ -341,7 +342,8 @@ def csum_chain(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch.Tens
         st = lib.rns_csum_chain_dev(arena.data_ptr(), arena.numel(), frag_off.data_ptr(), frag_len.data_ptr(), nf,
                                     first.data_ptr(), seed_ptr, out.data_ptr(), n,
                                     (_lib.RNS_FLAG_COMPLEMENT if complement else 0) |
-                                    (_lib.RNS_FLAG_CHAIN_RUNS if runs else 0), frag_len_hint,
+                                    (_lib.RNS_FLAG_CHAIN_RUNS if runs else 0) |
+                                    (_lib.RNS_FLAG_CHAIN_TX_PACKED if tx_packed else 0), frag_len_hint,
                                     frag_sums.data_ptr() if frag_sums is not None else None, bad_ptr,
                                     _stream_handle(dev))
     _lib.check(st, "rns_csum_chain_dev")
@@ -351,12 +353,14 @@ def csum_chain(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch.Tens
 def csum_chain_fill(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch.Tensor, first: torch.Tensor,
                     seed: torch.Tensor | None = None, *, field: torch.Tensor | None = None, field_off: int = 16,
                     complement: bool = True, out: torch.Tensor | None = None, bad: torch.Tensor | None = None,
-                    frag_len_hint: int = 512, runs: bool = False) -> torch.Tensor | None:
+                    frag_len_hint: int = 512, runs: bool = False, tx_packed: bool = False) -> torch.Tensor | None:
     """Transmit fill over fragment chains (rns_csum_chain_fill_dev): packet i = fragments
     ``first[i] .. first[i+1]`` as for ``csum_chain``; its checksum field is at byte
     ``field[i]`` (or ``field_off``) of its FIRST fragment (the head fragment
     alloc_header prepended, buf.rs:262-291), counts as zero, and receives
     ``compute_buffer_ones_comp(seed, chain) ^ 0xffff`` big-endian (tcp.rs:957-973).
+    ``tx_packed``: RNS_FLAG_CHAIN_TX_PACKED, the hint that packets are [head <= 4 chunks,
+    payload run] with the payloads packed at 16-byte starts (same results either way).
     Returns ``out`` if given."""
     _require_cuda(arena, "arena", (torch.uint8,))
     _require_cuda(frag_off, "frag_off", (torch.int64,))
@@ -387,7 +391,8 @@ def csum_chain_fill(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch
     if bad is not None:
         _require_cuda(bad, "bad", (torch.int32,))
         bad_ptr = bad.data_ptr()
-    flags = (_lib.RNS_FLAG_COMPLEMENT if complement else 0) | (_lib.RNS_FLAG_CHAIN_RUNS if runs else 0)
+    flags = (_lib.RNS_FLAG_COMPLEMENT if complement else 0) | (_lib.RNS_FLAG_CHAIN_RUNS if runs else 0) | \
+        (_lib.RNS_FLAG_CHAIN_TX_PACKED if tx_packed else 0)
     with torch.cuda.device(dev):
         st = _lib.load().rns_csum_chain_fill_dev(arena.data_ptr(), arena.numel(), frag_off.data_ptr(),
                                                  frag_len.data_ptr(), nf, first.data_ptr(), ptrs[0], ptrs[1],

@@ -32,7 +32,25 @@ int launch_chain(const CsumArgs &a, uint32_t K, bool nt, bool runs, hipStream_t 
     return hip_status(hipGetLastError());
 }
 
+// RNS_FLAG_CHAIN_TX_PACKED: the transmit-rows kernel (one wave per 64 packets).
+#ifndef RNS_TXROWS_D  // payload rows in flight per wave
+#define RNS_TXROWS_D 8
+#endif
+template <bool FILL>
+int launch_txrows(const CsumArgs &a, hipStream_t st)
+{
+    constexpr bool NT = RNS_STREAM_NT != 0;
+    const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);
+    if (buf_records(a) < kOobOffset)
+        hipLaunchKernelGGL((csum_txrows_kernel<NT, true, RNS_TXROWS_D, FILL>), grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL((csum_txrows_kernel<NT, false, RNS_TXROWS_D, FILL>), grid, block, 0, st, a);
+    return hip_status(hipGetLastError());
+}
+
 template int launch_chain<false>(const CsumArgs &, uint32_t, bool, bool, hipStream_t);
 template int launch_chain<true>(const CsumArgs &, uint32_t, bool, bool, hipStream_t);
+template int launch_txrows<false>(const CsumArgs &, hipStream_t);
+template int launch_txrows<true>(const CsumArgs &, hipStream_t);
 
 }  // namespace rns

@@ -11,13 +11,26 @@ namespace rns {
 // kernels carry no packed-form code): the mixed kernel, or for tiny packets the
 // rounds kernel with pick_shape's G=4, U=1 shape.
 // Receive verify's stream launch: one wave per 64-datagram unit.
+#ifndef RNS_RX_ROWS  // A/B knob (round 5): 1 = receive verify through the rows kernel, 0 = the stream kernel
+#define RNS_RX_ROWS 1
+#endif
+#ifndef RNS_RX_ROWS_D  // rows in flight of the receive form
+#define RNS_RX_ROWS_D 8
+#endif
 int launch_stream_rx(const CsumArgs &a, hipStream_t st)
 {
     const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);
-    if (buf_records(a) < kOobOffset)
-        hipLaunchKernelGGL((csum_stream_kernel<RNS_STREAM_NT != 0, true>), grid, block, 0, st, a);
-    else
-        hipLaunchKernelGGL((csum_stream_kernel<RNS_STREAM_NT != 0, false>), grid, block, 0, st, a);
+    constexpr bool NT = RNS_STREAM_NT != 0;
+    if (RNS_RX_ROWS) {
+        if (buf_records(a) < kOobOffset)
+            hipLaunchKernelGGL((csum_rows_rx_kernel<NT, true, RNS_RX_ROWS_D>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_rows_rx_kernel<NT, false, RNS_RX_ROWS_D>), grid, block, 0, st, a);
+    } else if (buf_records(a) < kOobOffset) {
+        hipLaunchKernelGGL((csum_stream_kernel<NT, true>), grid, block, 0, st, a);
+    } else {
+        hipLaunchKernelGGL((csum_stream_kernel<NT, false>), grid, block, 0, st, a);
+    }
     return hip_status(hipGetLastError());
 }
 
@@ -30,10 +43,9 @@ int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
     // 344.4-345.1 vs 346.4-347.1 (group kernel, u32 offsets), IMIX 451-453 vs 456 (round 3's
     // stream kernel).  Tiny packets keep the rounds kernel (c2: 13.2-13.7 vs 14.0-14.8 us with
     // round 3's stream kernel).
-#ifndef RNS_PACKED_TINY_ROUNDS  // A/B knob: 0 = tiny packets through the rows kernel too
-#define RNS_PACKED_TINY_ROUNDS 1
-#endif
-    const bool tiny = RNS_PACKED_TINY_ROUNDS && (sh.variant & ~16u) == 3u && sh.G == 4u && sh.U == 1u;
+    // (tiny packets through the rows kernel: c2 19.6 vs 13.8 us per isolated dispatch, a 4 KiB unit
+    // is all prologue: profiles/r04_unit_size_and_tiny.json)
+    const bool tiny = (sh.variant & ~16u) == 3u && sh.G == 4u && sh.U == 1u;
     if (a.align_mask >= 15u && !tiny) {
         constexpr bool NT = RNS_STREAM_NT != 0;
         const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);
@@ -68,11 +80,8 @@ int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
                                a);
     } else if ((sh.variant & ~16u) == 3u && sh.G == 4u && sh.U == 1u) {  // c2: 13.46 -> 13.36 us with prefetch
         const bool pf = (sh.variant & 16u) != 0;
-#ifndef RNS_PACKED_TINY_D  // A/B knob: 4 = every round of a wave batch issued at once (with the prefetch)
-#define RNS_PACKED_TINY_D 1
-#endif
         if (buf && pf)
-            hipLaunchKernelGGL((csum_rounds_kernel<4, 1, false, true, true, RNS_PACKED_TINY_D, true, true>), grid, block, 0,
+            hipLaunchKernelGGL((csum_rounds_kernel<4, 1, false, true, true, 1, true, true>), grid, block, 0,
                                st, a);
         else if (buf)
             hipLaunchKernelGGL((csum_rounds_kernel<4, 1, false, true, true, 1, true>), grid, block, 0, st, a);

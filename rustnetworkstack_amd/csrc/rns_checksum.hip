@@ -214,6 +214,10 @@ static int chain_launch(CsumArgs &a, const uint64_t *d_frag_off, const uint32_t 
                         const uint32_t *d_first, uint32_t n_pkts, uint32_t flags, uint32_t frag_len_hint,
                         hipStream_t stream)
 {
+    // the chain kernel adds packet indices in 32 bits (a VGPR less across its class pass): its
+    // last wave's base + 64 * K + lane must not wrap
+    if (n_pkts > 0xFFFFFFFFu - 64u * kChainMaxK)
+        return RNS_E_INVALID;
     a.off = d_frag_off;
     a.len = d_frag_len;
     a.n = n_pkts;
@@ -234,6 +238,8 @@ static int chain_launch(CsumArgs &a, const uint64_t *d_frag_off, const uint32_t 
         }
     }
     a.chain_k = K;
+    if (flags & RNS_FLAG_CHAIN_TX_PACKED)  // transmit-shaped chains: heads + a packed payload region
+        return launch_txrows<FILL>(a, stream);
     // Nontemporal loads for NetBuffer-sized fragments (c3 as 3 fragments: 298 -> 289 us
     // packed back to back, 281 -> 261 us in 512-byte buffers), not for IMIX's mix of
     // 40-byte packets and 512-byte fragments (646 -> 670 us): profiles/archive/r02/r02_chain_ab.json.

@@ -694,15 +694,10 @@ __global__ __launch_bounds__(kBlock) void csum_rounds_kernel(const CsumArgs a)
                 v[u] = w[u];
         }
         const uint16_t acc = finalize(mine, d_start, d_len, d_seed, d_ok, a.flags);
-#ifndef RNS_ROUNDS_NTSTORE  // A/B knob: nontemporal result stores in the rounds kernel
-#define RNS_ROUNDS_NTSTORE 0
-#endif
-        if (live) {
-            if constexpr (RNS_ROUNDS_NTSTORE != 0)
-                __builtin_nontemporal_store(static_cast<uint16_t>(acc), a.out + p);
-            else
-                a.out[p] = static_cast<uint16_t>(acc);  // 64 consecutive u16: one 128-byte store
-        }
+        // 64 consecutive u16: one 128-byte store (nontemporal stores measured 12.88 -> 13.21 us on
+        // c2, r03; the ordinary policy stays)
+        if (live)
+            a.out[p] = static_cast<uint16_t>(acc);
         if (a.bad) {
             const uint64_t rejected = __ballot(live && !d_ok);
             if (rejected && lane == 0)
@@ -829,21 +824,9 @@ __device__ __forceinline__ FillSite fill_site(const CsumArgs &a, uint64_t d_star
     return f;
 }
 
-// A/B knob: the transmit stores with the nontemporal cache policy.
-#ifndef RNS_FILL_NTSTORE
-#define RNS_FILL_NTSTORE 0
-#endif
-__device__ __forceinline__ void store_block(uint4 *p, uint4 v)
-{
-    if constexpr (RNS_FILL_NTSTORE != 0) {
-        __builtin_nontemporal_store(v.x, &p->x);
-        __builtin_nontemporal_store(v.y, &p->y);
-        __builtin_nontemporal_store(v.z, &p->z);
-        __builtin_nontemporal_store(v.w, &p->w);
-    } else {
-        *p = v;
-    }
-}
+// A transmit block store: the ordinary cache policy (nontemporal stores were 11-25 % slower:
+// the scattered writes gain from being combined in the caches, profiles/archive/r02/r02_fill_ntstore_ab.json).
+__device__ __forceinline__ void store_block(uint4 *p, uint4 v) { *p = v; }
 
 // set_be16(&mut header[f..f+2], checksum): rewrite the block from the stash (stp =
 // the packet's stash chunks) with the field patched in, or store the two bytes.
@@ -1578,11 +1561,9 @@ csum_mixed_kernel(const CsumArgs a)
                 load_next(base + wstep);  // in flight while this batch finishes and stores
         }
         const uint16_t res = finalize_bits(mine, odd, big, d_seed, d_ok, a.flags);
-#ifndef RNS_MIXED_NTSTORE  // nontemporal result stores in the plain class kernel (c3 232.4 -> 229.5 us per step, r03l)
-#define RNS_MIXED_NTSTORE 1
-#endif
         if (live && a.out) {
-            if constexpr (RNS_MIXED_NTSTORE != 0 && !FILL && !RX && !TX)
+            // nontemporal result stores in the plain class kernel (c3 232.4 -> 229.5 us per step, r03l)
+            if constexpr (!FILL && !RX && !TX)
                 __builtin_nontemporal_store(res, a.out + p);
             else
                 a.out[p] = res;  // 64 consecutive u16: one 128-byte store
@@ -1695,9 +1676,21 @@ __device__ __forceinline__ uint32_t fragment_run(const CsumArgs &a, uint32_t f0,
     return run && tot <= kNoWrapBytes ? tot : kNoRun;
 }
 
-#ifndef RNS_CHAIN_OCC
-#define RNS_CHAIN_OCC 4
+// Waves/SIMD of the chain kernel: 4 (128 VGPRs) where the instantiation fits them with no
+// scratch — the nontemporal buffer forms of the plain checksum (NetBuffer-sized fragments: c3
+// chains 4-7 % faster than at 3, session r04b) — and 3 (168 VGPRs) for the rest, which spill
+// 8-52 B/lane at 4 (the temporal class pass with its tiny class, the 64-bit addresses of
+// arenas of 4 GiB and more, the fill's extra state; profiles/r05_resources.txt).
+// -DRNS_CHAIN_OCC=n forces n for every instantiation (A/B builds).
+template <bool NT, bool BUF, uint32_t KMAX, bool RUNS, bool FILL>
+constexpr int chain_occ()
+{
+#ifdef RNS_CHAIN_OCC
+    return RNS_CHAIN_OCC;
+#else
+    return (NT && BUF && !FILL && !(RUNS && KMAX > 1)) ? 4 : 3;
 #endif
+}
 // Workgroup size of the chain kernel: one wave.  Its per-packet state is LDS, which is
 // freed per workgroup, as for the mixed kernel's stash modes: IMIX chains 640 -> 608 us
 // packed, 839 -> 771 us in 512-byte buffers, c3 equal (profiles/r02_block_ab.json).
@@ -1719,7 +1712,7 @@ constexpr int kChainBlock = RNS_CHAIN_BLOCK;
 // packet whose head fragment cannot hold its field (or has no fragments) is rejected:
 // result 0, counted, nothing stored.
 template <bool NT, bool BUF, uint32_t KMAX, bool RUNS = false, bool FILL = false>
-__global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(const CsumArgs a)
+__global__ __launch_bounds__(kChainBlock, (chain_occ<NT, BUF, KMAX, RUNS, FILL>())) void csum_chain_kernel(const CsumArgs a)
 {
     static_assert(!RUNS || BUF, "runs: buffer path only");
     // A wave owns K*64 consecutive packets (K = a.chain_k, chosen by the host from the
@@ -1754,7 +1747,7 @@ __global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(
         uint32_t lo_all = 0xFFFFFFFFu, hi_all = 0u;
         bool runs_all = true;
         for (uint32_t q = 0; q < K; ++q) {
-            const uint64_t p = static_cast<uint64_t>(base) + q * 64 + lane;  // (widened before the add)
+            const uint64_t p = base + q * 64 + lane;  // (32-bit add: the host caps a.n at 2^32 - 64 * kChainMaxK)
             const bool live = p < a.n;
             uint32_t f0 = live ? a.first[p] : 0u, f1 = live ? a.first[p + 1] : 0u;
             const bool ok = f0 <= f1 && f1 <= a.n_frags;
@@ -1877,7 +1870,7 @@ __global__ __launch_bounds__(kChainBlock, RNS_CHAIN_OCC) void csum_chain_kernel(
         }
         wave_lds_fence();
         for (uint32_t q = 0; q < K; ++q) {
-            const uint64_t p = static_cast<uint64_t>(base) + q * 64 + lane;
+            const uint64_t p = base + q * 64 + lane;
             const uint32_t acc = pk[2][q * 64 + lane];
             uint32_t r = acc & 0xffffu;
             if (a.flags & RNS_FLAG_COMPLEMENT)
@@ -2221,24 +2214,31 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
     }
 }
 
-#ifndef RNS_ROWS_END_LATE  // the owner's end-chunk load issued a group of rows ahead of its row, not up
-#define RNS_ROWS_END_LATE 1  // front (c3 isolated 228.2-229.4 -> 224.8 us, traffic 1.030 -> 1.006x; session r04q)
-#endif
-#ifndef RNS_ROWS_LINE_ALIGN  // rows start at the 128-byte line below the region (IMIX 445.8-446.0 ->
-#define RNS_ROWS_LINE_ALIGN 1  // 436.6-437.5 us, 0.809 -> 0.825, traffic 1.042 -> 1.034x; session r04w)
-#endif
-#ifndef RNS_ROWS_TAIL_MASK  // lanes past the region's end in its last row load nothing (IMIX isolated
-#define RNS_ROWS_TAIL_MASK 1  // 451.7-453.3 -> 447.9-448.4 us, traffic 1.062 -> 1.042x; session r04r)
-#endif
+// Three measured choices shape the row stream (round 4; the losing forms are gone):
+//  * the owner's end-chunk load is issued a group of rows ahead of its row, not up front
+//    (c3 isolated 228.2-229.4 -> 224.8 us, traffic 1.030 -> 1.006x; session r04q);
+//  * rows start at the 128-byte line below the region (IMIX 445.8-446.0 -> 436.6-437.5 us,
+//    0.809 -> 0.825, traffic 1.042 -> 1.034x; session r04w);
+//  * lanes past the region's end in its last row load nothing (IMIX isolated 451.7-453.3 ->
+//    447.9-448.4 us, traffic 1.062 -> 1.042x; session r04r).
 // The rows decomposition over one region that starts 16-byte aligned at r0 (an offset from
 // a.arena) and holds total bytes (a multiple of 16; ceil(total / 1 KiB) rows): the lane's packet covers chunks c0..e of the region (its
 // start 16-byte aligned, len bytes, len 0: none).  Returns the packet's LE word sum (pairs by
 // absolute parity).  csum_rows_kernel's aligned path and the chain kernel's runs (below).
-template <bool NT, bool BUF, int D>
+struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
+// `after_first` runs once the first D rows are issued (a caller's own earlier loads are then
+// the oldest in flight: consuming them waits for exactly those, not for the rows).
+// NH > 0 (receive verify): the owner also loads its packet's first NH chunks into hv[] (those
+// inside the packet; the others read as zero), like its end chunk: a group of rows ahead of
+// the row that streams them, so each line is fetched once.
+template <bool NT, bool BUF, int D, int NH = 0, typename Hook = NoHook>
 __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __amdgpu_buffer_rsrc_t rsrc, uint64_t recs,
-                                                   uint64_t r0, uint32_t total, uint32_t c0, uint32_t e, uint32_t len)
+                                                   uint64_t r0, uint32_t total, uint32_t c0, uint32_t e, uint32_t len,
+                                                   uint4 *hv = nullptr, Hook after_first = Hook{})
 {
-    if constexpr (RNS_ROWS_LINE_ALIGN != 0) {
+    {
         // start the row stream at the 128-byte line below the region (the few bytes before it
         // belong to no packet of this unit; prefix differences cancel them), so every 1 KiB row
         // covers 8 whole lines, not 9 — IMIX regions end anywhere on a 16-byte boundary
@@ -2254,11 +2254,15 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
     // the owner's end chunk (pulling it from its row instead, four ds_bpermute per row, measured
     // 2x slower: session r04g)
     uint4 endv = make_uint4(0, 0, 0, 0);
-    constexpr bool kLate = BUF && RNS_ROWS_END_LATE != 0;
+    constexpr bool kLate = BUF;
     const uint32_t row_e = len ? e >> 6 : 0xFFFFFFFFu;
-    // RNS_ROWS_END_LATE: the owners load their end chunks a group of D rows ahead of the rows
+    // the owners load their end chunks a group of D rows ahead of the rows
     // that hold them (one exec-masked load per group: its line is then still in L2 when the row
     // streams it), not all before the first row
+    const uint32_t row_h = len ? c0 >> 6 : 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i < NH; ++i)
+        hv[i] = make_uint4(0, 0, 0, 0);
     auto load_end_late = [&](uint32_t k) {  // end chunks in rows [k, k + D)
         if constexpr (kLate) {
             if (row_e - k < static_cast<uint32_t>(D)) {
@@ -2266,9 +2270,23 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
                 const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16u <= recs ? off : kOobOffset, 0, 0);
                 endv = make_uint4(x.x, x.y, x.z, x.w);
             }
+            if constexpr (NH > 0) {  // the packet's first chunks, a group ahead of their row
+                if (row_h - k < static_cast<uint32_t>(D)) {
+#pragma unroll
+                    for (int i = 0; i < NH; ++i) {
+                        const uint32_t off = static_cast<uint32_t>(r0) + ((c0 + i) << 4);
+                        const bool in = 16u * i < len && off + 16u <= recs;
+                        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, in ? off : kOobOffset, 0, 0);
+                        hv[i] = make_uint4(x.x, x.y, x.z, x.w);
+                    }
+                }
+            }
         }
     };
     if constexpr (!kLate) {
+#pragma unroll
+        for (int i = 0; i < NH; ++i)
+            hv[i] = own_chunk<BUF>(a, rsrc, recs, r0 + (static_cast<uint64_t>(c0) << 4), len, i);
         const uint64_t off = r0 + (static_cast<uint64_t>(e) << 4);
         const bool in = len != 0 && off + 16 <= recs;
         if constexpr (BUF) {
@@ -2285,16 +2303,10 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
     uint4 v[D];
     auto issue = [&](uint32_t k, uint4 &dst) {  // row k: chunk 64k + lane of the region
         if constexpr (BUF) {
-            // wave-uniform row base (a row past the region: out of range, no traffic)
-            uint32_t o;
-            if constexpr (RNS_ROWS_TAIL_MASK != 0) {
-                // lanes past the region's end load nothing (the next unit's wave streams those
-                // bytes, often on another XCD's L2)
-                const uint32_t rel = (k << 10) + vlane;
-                o = rel < total ? static_cast<uint32_t>(r0) + rel : kOobOffset;
-            } else {
-                o = (k < nrows ? static_cast<uint32_t>(r0) + (k << 10) : kOobOffset) + vlane;
-            }
+            // lanes past the region's end load nothing (a row past it: no traffic at all); the next
+            // unit's wave streams those bytes, often on another XCD's L2
+            const uint32_t rel = (k << 10) + vlane;
+            const uint32_t o = rel < total ? static_cast<uint32_t>(r0) + rel : kOobOffset;
             const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, NT ? kNtAux : 0);
             dst = make_uint4(x.x, x.y, x.z, x.w);
         } else {
@@ -2310,6 +2322,8 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
         issue(j, v[j]);
         __builtin_amdgcn_sched_barrier(0);
     }
+    after_first();
+    __builtin_amdgcn_sched_barrier(0);
     // the owner's partial end chunk (its padding bytes never count)
     auto end_part = [&]() -> uint32_t {
         uint32_t part = 0;
@@ -2372,9 +2386,8 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
 // (P(-1) = 0; e == c0: the end chunk alone).  The owner lane pulls P(c0 - 1) and
 // P(e - 1) from the lanes that hold them with ds_bpermute in the rows they fall in, and
 // loads its end chunk itself one group of D rows before the row that streams it (the line
-// is fetched once: RNS_ROWS_END_LATE), so the end chunk's padding bytes never need a
-// per-row mask.  Rows start at the 128-byte line below the region (RNS_ROWS_LINE_ALIGN) and
-// lanes past its end load nothing (RNS_ROWS_TAIL_MASK).  Per KiB: 4 sad + the scan + two captures, no LDS memory, no fences
+// is fetched once), so the end chunk's padding bytes never need a per-row mask.  Rows start
+// at the 128-byte line below the region and lanes past its end load nothing.  Per KiB: 4 sad + the scan + two captures, no LDS memory, no fences
 // (csum_stream_kernel: a table publish, two wave fences, the masks; 57 VALU/KB).
 // u32 differences are exact: a packet's LE word sum is < 2^32.
 // ---------------------------------------------------------------------------
@@ -2552,6 +2565,376 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : FILL ? RNS_ROWS_FILL_OCC : 8) voi
     }
     if (a.bad) {
         const uint64_t rejected = __ballot(live && !(ok && (!FILL || fok)));
+        if (rejected && lane == 0)
+            atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Receive verify through the rows decomposition (rns_rx_verify_packed_dev, round 5):
+// ip_input_v4 (ip.rs:65-92), ip_input_v6 (ip.rs:114-121), tcp::validate_checksum
+// (tcp.rs:838-850), icmp_input_v4/v6 (icmp.rs:44-75) over a packed arena of datagrams.  The
+// whole datagram's word sum T comes from csum_rows_kernel's rows (P(e-1) - P(c0-1) + the
+// owner's end chunk: no LDS table, no fences); each owner also loads its datagram's first 4
+// chunks (64 bytes: every IPv4 header incl. options, the IPv6 header) a group of rows ahead
+// of the row that streams them, as it loads its end chunk, and finishes exactly as the class
+// kernel's receive verify does (rx_finish: header sum H, pseudo-header from the header's own
+// addresses, L4 = T - H).  A unit of ACK-sized datagrams (all <= 64 B) skips the rows: each
+// owner loads its datagram whole; a unit that does not start 16-byte aligned takes the
+// per-datagram wave loop.
+// ---------------------------------------------------------------------------
+#ifndef RNS_ROWS_RX_OCC  // waves/SIMD bound of the receive form (its header chunks need registers)
+#define RNS_ROWS_RX_OCC 5
+#endif
+template <bool NT, bool BUF, int D>
+__global__ __launch_bounds__(64, RNS_ROWS_RX_OCC) void csum_rows_rx_kernel(const CsumArgs a)
+{
+    constexpr int kNS = 4;  // header chunks per datagram (16-byte-aligned: its first 64 bytes)
+    const uint32_t lane = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
+    const uint64_t recs = buf_records(a);
+    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * 64;
+    const uint64_t p = base + lane;
+    const bool live = p < a.n;
+    const uint64_t q = live ? p : a.n - 1;  // branch-free descriptor loads
+    const uint32_t zero_v = __builtin_amdgcn_mbcnt_lo(0u, 0u);
+    const uint64_t r0v = a.blk_off[(base >> 6) + zero_v];
+    const uint32_t len = live ? static_cast<uint32_t>(a.len16[q]) : 0u;
+    const uint64_t r0 =
+        ((static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(r0v >> 32))))
+          << 32) |
+         static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(r0v)))) +
+        a.base_adjust;  // the wave's first datagram
+    const uint32_t pad = (len + a.align_mask) & ~a.align_mask;
+    const uint32_t incl = wave_incl_scan(pad);
+    const uint32_t excl = incl - pad;
+    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);  // the region's bytes
+    const uint64_t start = r0 + excl;
+    const bool ok = start <= a.arena_bytes && len <= a.arena_bytes - start;
+    uint32_t mine = 0;
+    uint4 own[kNS + 1];
+    own[kNS] = make_uint4(0, 0, 0, 0);
+    uint32_t s0 = 0;
+    bool odd = false;
+    if ((r0 & 15) == 0 && !__ballot(len > 64)) {
+        // ---- ACK-sized unit: every owner takes its datagram whole ----
+#pragma unroll
+        for (int i = 0; i < kNS; ++i)  // all four loads in flight before the first is used
+            own[i] = own_chunk<BUF>(a, rsrc, recs, start, len, i);
+#pragma unroll
+        for (int i = 0; i < kNS; ++i) {
+            uint4 x = own[i];
+            if (16u * i + 16u > len)  // rx_finish sees zeros past the end
+                x = 16u * i < len ? keep_first(x, len - 16u * i) : make_uint4(0, 0, 0, 0);
+            own[i] = x;
+            mine = __builtin_amdgcn_sad_u16(x.x, 0, mine);
+            mine = __builtin_amdgcn_sad_u16(x.y, 0, mine);
+            mine = __builtin_amdgcn_sad_u16(x.z, 0, mine);
+            mine = __builtin_amdgcn_sad_u16(x.w, 0, mine);
+        }
+    } else if ((r0 & 15) == 0) {
+        // ---- the rows: T, and the owner's first 4 chunks loaded a group ahead ----
+        const uint32_t c0 = excl >> 4;
+        const uint32_t e = len ? (excl + len - 1) >> 4 : c0;
+        mine = rows_region_sum<NT, BUF, D, kNS>(a, rsrc, recs, r0, total, c0, e, len, own);
+#pragma unroll
+        for (int i = 0; i < kNS; ++i)  // zeros past the datagram's end (the region's next bytes)
+            if (16u * i + 16u > len)
+                own[i] = 16u * i < len ? keep_first(own[i], len - 16u * i) : make_uint4(0, 0, 0, 0);
+    } else {
+        // ---- unaligned region (rare): the whole wave sums one datagram at a time ----
+        uint64_t todo = __ballot(len != 0 && ok);
+        while (todo) {
+            const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
+            todo &= todo - 1;
+            const uint64_t st =
+                (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start >> 32), o)))
+                 << 32) |
+                static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start), o));
+            const uint32_t L = __builtin_amdgcn_readlane(len, o);
+            const Pkt k = make_pkt(st, L);
+            uint32_t acc = 0;
+            for (uint32_t cc = 0; cc < k.nch; cc += 64) {
+                uint4 w[1];
+                issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, w);
+                mask_edges<64, 1, 1>(k, cc + lane, w);
+                acc = sum_le<1, 1>(w, acc);
+            }
+            const uint32_t sum = group_allreduce<64>(acc);
+            mine = lane == o ? sum : mine;
+        }
+        odd = r0 & 1;  // every datagram of the range shares the region start's misalignment
+        // each owner takes its header from the 16-byte boundary below its start: 5 chunks hold
+        // its first 65-80 bytes, masked to the datagram
+        const uint64_t b0 = start & ~15ull;
+        s0 = static_cast<uint32_t>(start & 15);
+#pragma unroll
+        for (int i = 0; i < kNS + 1; ++i)
+            own[i] = own_chunk<BUF>(a, rsrc, recs, b0, (len && ok) ? s0 + len : 0u, i);
+#pragma unroll
+        for (int i = 0; i < kNS + 1; ++i) {
+            const int lo = static_cast<int>(s0) - 16 * i, hi = static_cast<int>(s0 + len) - 16 * i;
+            own[i] = make_uint4(keep_bytes(own[i].x, lo, hi, 0), keep_bytes(own[i].y, lo, hi, 4),
+                                keep_bytes(own[i].z, lo, hi, 8), keep_bytes(own[i].w, lo, hi, 12));
+        }
+    }
+    uint32_t l4_res = 0;
+    const uint8_t stv = rx_finish<kNS + 1>(a, own, mine, s0, len, odd, false, live && ok && len != 0, l4_res);
+    if (live) {
+        a.status[p] = stv;
+        if (a.l4_out)
+            a.l4_out[p] = static_cast<uint16_t>(l4_res);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Transmit-shaped chains (RNS_FLAG_CHAIN_TX_PACKED; rns_csum_chain_dev and
+// rns_csum_chain_fill_dev).  What tcp_output checksums (tcp.rs:938-973) is a head fragment
+// (the TCP header alloc_header prepended, buf.rs:262-291) followed by the payload.  A batching
+// transmit path keeps the heads of consecutive packets back to back in a header region and the
+// payloads back to back, 16-byte aligned, in a payload region.  Then a wave's 64 payloads are
+// ONE region and stream as csum_rows_kernel's rows (P(e-1) - P(c0-1) + the owner's end chunk),
+// while each owner loads its own head (at most 4 chunks; the 64 heads of a wave are one
+// contiguous run, so those loads coalesce) and, for the fill, stores its field into it:
+// 64 two-byte stores into one short run of lines instead of 64 scattered writes.
+//
+// The chain is folded as compute_buffer_ones_comp does (util.rs:112-119): acc = fold(seed +
+// G(head)), then fold(acc + G(payload)) — the payload's fragments form a run (back to back,
+// even non-final lengths: their words pair as one slice's), so the payload is
+// one contiguous sum; G(x) is the folded sum in big-endian order (zero iff all bytes zero).
+// With the fill the field's two bytes are taken out of the head's exact sum before the fold.
+//
+// Every lane classifies its packet from its first 1 + kRunFrags descriptors (one round of
+// loads after first[]).  A wave whose packets all have that shape (or a defined rejection:
+// malformed range, no fragments, a fragment outside the arena, a head too short for its
+// field) and whose payloads ascend at 16-byte starts with bounded gaps takes the rows; any
+// other wave takes an exact per-packet loop (the whole wave sums one fragment at a time,
+// big-endian words mod 2^32: util.rs:88-106 literally), so the hint never changes a result.
+// ---------------------------------------------------------------------------
+#ifndef RNS_TXROWS_OCC  // waves/SIMD bound of the transmit-rows kernel
+#define RNS_TXROWS_OCC 5  // (zero scratch at 86-89 VGPRs; 6 spills 32-116 B/lane)
+#endif
+constexpr uint32_t kTxHeadMax = 64;  // (head start & 15) + head length: at most 4 chunks
+
+// Inclusive max over the 64 lanes (Hillis-Steele over DPP row shifts, then the row broadcasts).
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v)
+{
+    uint32_t x = v;
+    x = max(x, dpp_or_zero<0x111>(x));           // row_shr:1
+    x = max(x, dpp_or_zero<0x112>(x));           // row_shr:2
+    x = max(x, dpp_or_zero<0x114>(x));           // row_shr:4
+    x = max(x, dpp_or_zero<0x118>(x));           // row_shr:8
+    x = max(x, dpp_or_zero<0x142, 0xA, 0xF>(x));  // row_bcast:15 into rows 1 and 3
+    x = max(x, dpp_or_zero<0x143, 0xC, 0xF>(x));  // row_bcast:31 into rows 2 and 3
+    return x;
+}
+
+__device__ __forceinline__ uint32_t bswap16_u32(uint32_t x) { return ((x & 0xff) << 8) | (x >> 8); }
+
+template <bool NT, bool BUF, int D, bool FILL>
+__global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const CsumArgs a)
+{
+    const uint32_t lane = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
+    const uint64_t recs = buf_records(a);
+    const uint64_t p = static_cast<uint64_t>(blockIdx.x) * 64 + lane;
+    const bool live = p < a.n;
+    const uint32_t f0 = live ? a.first[p] : 0u, f1 = live ? a.first[p + 1] : 0u;
+    const bool rng_ok = f0 <= f1 && f1 <= a.n_frags;
+    const uint32_t nfr = live && rng_ok ? f1 - f0 : 0u;
+    const uint32_t seed = (a.seed && live) ? static_cast<uint32_t>(a.seed[p]) : 0u;
+    uint32_t fo = 0;
+    if constexpr (FILL)
+        fo = live ? (a.field ? static_cast<uint32_t>(a.field[p]) : a.field_off) : 0u;
+    // the head and up to kRunFrags payload fragments: one round of descriptor loads
+    constexpr uint32_t kF = 1 + kRunFrags;
+    uint64_t o[kF];
+    uint32_t l[kF];
+#pragma unroll
+    for (uint32_t j = 0; j < kF; ++j) {
+        o[j] = 0;
+        l[j] = 0;
+        if (j < nfr) {
+            o[j] = a.off[f0 + j] + a.base_adjust;
+            l[j] = a.len[f0 + j];
+        }
+    }
+    bool all_in = true, run = nfr <= kF;
+    uint32_t plen = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kF; ++j) {
+        if (j < nfr) {
+            const bool in = o[j] <= a.arena_bytes && l[j] <= a.arena_bytes - o[j];
+            all_in = all_in && in;
+            if (j >= 1) {
+                run = run && (j == 1 || (o[j] == o[j - 1] + l[j - 1] && !(l[j - 1] & 1u)));
+                plen += l[j];
+            }
+        }
+    }
+    const uint32_t hl = l[0];
+    // defined rejections (every path): bad range, no fragments, a fragment outside the arena,
+    // a head too short for the field — the packet gets 0, is counted and is left untouched
+    bool bad = live && (!rng_ok || nfr == 0 || (nfr <= kF && !all_in));
+    if constexpr (FILL)
+        bad = bad || (live && nfr != 0 && !(fo <= hl && hl - fo >= 2u));
+    const bool has_pay = live && !bad && plen != 0;
+    const uint64_t po = o[1];
+    const bool shape = !live || bad ||
+                       (run && plen <= 0xFFFFu && (o[0] & 15u) + hl <= kTxHeadMax && (!has_pay || (po & 15u) == 0));
+    // the wave's payload region: ascending, 16-byte starts, gaps bounded (else the exact loop)
+    const uint64_t pm = __ballot(has_pay);
+    uint64_t r0 = 0;
+    uint32_t rel = 0, c0 = 0, e = 0, total = 0;
+    bool region = true;
+    if (pm) {
+        const uint32_t fl = static_cast<uint32_t>(__builtin_ctzll(pm));
+        r0 = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(po >> 32), fl)))
+              << 32) |
+             static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(po), fl));
+        const uint64_t rel64 = has_pay ? po - r0 : 0;
+        const uint32_t pad = has_pay ? (plen + 15u) & ~15u : 0u;
+        const bool near = rel64 < (1ull << 30);
+        rel = static_cast<uint32_t>(rel64);
+        const uint32_t end = has_pay && near ? rel + pad : 0u;
+        const uint32_t incl = wave_incl_max(end);
+        const uint32_t before = static_cast<uint32_t>(__shfl(static_cast<int>(incl), static_cast<int>(lane) - 1, 64));
+        const bool asc = !has_pay || (near && (lane == 0 || rel >= before));
+        total = __builtin_amdgcn_readlane(incl, 63);
+        const uint32_t sum_pad = __builtin_amdgcn_readlane(wave_incl_scan(pad), 63);
+        region = !__ballot(!asc) && total <= 2u * sum_pad + 4096u;
+        c0 = has_pay ? rel >> 4 : 0u;
+        e = has_pay ? (rel + plen - 1u) >> 4 : 0u;
+    }
+    const bool fast = !__ballot(!shape) && region;
+    uint32_t res = 0;  // the folded sum (before the complement)
+    if (fast) {
+        // the owner's head: its chunks issued before the rows, consumed after the first group
+        const uint64_t hb = o[0] & ~15ull;
+        const uint32_t hs = static_cast<uint32_t>(o[0] & 15u), span = live && !bad ? hs + hl : 0u;
+        uint4 h[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+            h[i] = own_chunk<BUF>(a, rsrc, recs, hb, span, i);
+        uint32_t acc1 = 0;
+        auto head = [&]() {
+            uint32_t hsum = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i) {
+                const int lo = static_cast<int>(hs) - 16 * static_cast<int>(i), hi = static_cast<int>(span) - 16 * static_cast<int>(i);
+                hsum = __builtin_amdgcn_sad_u16(keep_bytes(h[i].x, lo, hi, 0), 0, hsum);
+                hsum = __builtin_amdgcn_sad_u16(keep_bytes(h[i].y, lo, hi, 4), 0, hsum);
+                hsum = __builtin_amdgcn_sad_u16(keep_bytes(h[i].z, lo, hi, 8), 0, hsum);
+                hsum = __builtin_amdgcn_sad_u16(keep_bytes(h[i].w, lo, hi, 12), 0, hsum);
+            }
+            if constexpr (FILL) {  // the field counts as zero (buf.rs:286-288)
+                const uint32_t w[16] = {h[0].x, h[0].y, h[0].z, h[0].w, h[1].x, h[1].y, h[1].z, h[1].w,
+                                        h[2].x, h[2].y, h[2].z, h[2].w, h[3].x, h[3].y, h[3].z, h[3].w};
+                const uint32_t q0 = hs + fo, q1 = q0 + 1u;  // < 64 for a packet that is not rejected
+                uint32_t d0 = 0, d1 = 0;
+#pragma unroll
+                for (uint32_t d = 0; d < 16; ++d) {
+                    d0 = (q0 >> 2) == d ? w[d] : d0;
+                    d1 = (q1 >> 2) == d ? w[d] : d1;
+                }
+                const uint32_t b0 = (d0 >> ((q0 & 3u) * 8u)) & 0xffu, b1 = (d1 >> ((q1 & 3u) * 8u)) & 0xffu;
+                hsum -= (live && !bad) ? (b0 << ((q0 & 1u) * 8u)) + (b1 << ((q1 & 1u) * 8u)) : 0u;
+            }
+            const uint32_t x = fold16(hsum);
+            const uint32_t g = (o[0] & 1u) ? x : bswap16_u32(x);
+            const uint32_t t = seed + g;  // util.rs:89-103 with in_checksum = seed (no wrap: <= 0x1fffe)
+            acc1 = (t & 0xffff) + (t >> 16);
+        };
+        uint32_t mine = 0;
+        if (pm) {
+            mine = rows_region_sum<NT, BUF, D>(a, rsrc, recs, r0, total, c0, e, has_pay ? plen : 0u, nullptr, head);
+        } else {
+            head();
+        }
+        const uint32_t x = fold16(mine);
+        const uint32_t t = acc1 + bswap16_u32(x);  // the payload starts 16-byte aligned: even
+        res = has_pay ? (t & 0xffff) + (t >> 16) : acc1;
+    } else {
+        // ---- the exact per-packet loop: the whole wave sums one fragment at a time ----
+        uint64_t todo = __ballot(live && rng_ok && nfr != 0 && !bad);
+        bool lbad = bad;
+        while (todo) {
+            const uint32_t ow = static_cast<uint32_t>(__builtin_ctzll(todo));
+            todo &= todo - 1;
+            const uint32_t F0 = __builtin_amdgcn_readlane(f0, ow), F1 = __builtin_amdgcn_readlane(f1, ow);
+            const uint32_t FO = __builtin_amdgcn_readlane(fo, ow);
+            uint32_t acc = __builtin_amdgcn_readlane(seed, ow);
+            bool pbad = false;
+            for (uint32_t f = F0; f < F1; ++f) {
+                const uint64_t st = a.off[f] + a.base_adjust;
+                const uint32_t L = a.len[f];
+                if (!(st <= a.arena_bytes && L <= a.arena_bytes - st)) {
+                    pbad = true;
+                    break;
+                }
+                if (L == 0)  // an empty fragment adds nothing (the reference panics on it)
+                    continue;
+                const Pkt k = make_pkt(st, L);
+                const uint32_t w_hi = (st & 1) ? 0x01000100u : 0x00010001u;
+                const uint64_t fpos = st + FO;  // FILL: the field in the head fragment (f == F0)
+                uint32_t hsb = 0, lsb = 0;
+                for (uint32_t cc = 0; cc < k.nch; cc += 64) {
+                    uint4 w[1];
+                    issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, w);
+                    mask_edges<64, 1, 1>(k, cc + lane, w);
+                    if (FILL && f == F0) {
+                        const uint64_t cs = (st & ~15ull) + (static_cast<uint64_t>(cc + lane) << 4);
+                        const int lo = static_cast<int>(static_cast<int64_t>(fpos) - static_cast<int64_t>(cs));
+                        if (lo > -2 && lo < 16) {  // zero the field's bytes in this chunk
+                            // (keep_bytes keeps [lo, hi) of a dword: here everything but [lo, lo + 2))
+                            w[0].x &= ~keep_bytes(0xffffffffu, lo, lo + 2, 0);
+                            w[0].y &= ~keep_bytes(0xffffffffu, lo, lo + 2, 4);
+                            w[0].z &= ~keep_bytes(0xffffffffu, lo, lo + 2, 8);
+                            w[0].w &= ~keep_bytes(0xffffffffu, lo, lo + 2, 12);
+                        }
+                    }
+                    sum_be<1, 1>(w, w_hi, hsb, lsb);
+                }
+                const uint32_t words = group_allreduce<64>((hsb << 8) + lsb);  // BE words mod 2^32
+                acc += words;                                                   // util.rs:89-99
+                while (acc > 0xffff)                                            // util.rs:101-103
+                    acc = (acc & 0xffff) + (acc >> 16);
+            }
+            if (lane == ow) {
+                res = acc;
+                lbad = pbad;
+            }
+        }
+        bad = lbad;
+    }
+    const bool okp = live && !bad;
+    const uint32_t r = (a.flags & RNS_FLAG_COMPLEMENT) ? res ^ 0xffffu : res;
+    if constexpr (FILL) {
+        if (okp) {  // set_be16(&mut header[fo..fo + 2], result): the head fragment's bytes
+            uint8_t *w8 = const_cast<uint8_t *>(a.arena);
+            const uint64_t fp = o[0] + fo;
+            if (fp & 1) {
+                w8[fp] = static_cast<uint8_t>(r >> 8);
+                w8[fp + 1] = static_cast<uint8_t>(r);
+            } else {
+                *reinterpret_cast<uint16_t *>(w8 + fp) = static_cast<uint16_t>(bswap16_u32(r & 0xffffu));
+            }
+        }
+    }
+    if (live && a.out) {
+        const uint16_t v = okp ? static_cast<uint16_t>(r) : static_cast<uint16_t>(0);
+        if (a.n < (1u << 30)) {
+            const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+                static_cast<void *>(a.out), static_cast<short>(0), static_cast<int>(2u * a.n), 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b16(v, out_rsrc, static_cast<uint32_t>(2 * p), 0, RNS_STREAM_OUT_AUX);
+        } else {
+            __builtin_nontemporal_store(v, a.out + p);
+        }
+    }
+    if (a.bad) {
+        const uint64_t rejected = __ballot(live && !okp);
         if (rejected && lane == 0)
             atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
     }

@@ -79,6 +79,10 @@ template <bool FILL>
 int launch_chain(const CsumArgs &a, uint32_t K, bool nt, bool runs, hipStream_t st);
 extern template int launch_chain<false>(const CsumArgs &, uint32_t, bool, bool, hipStream_t);
 extern template int launch_chain<true>(const CsumArgs &, uint32_t, bool, bool, hipStream_t);
+template <bool FILL>
+int launch_txrows(const CsumArgs &a, hipStream_t st);
+extern template int launch_txrows<false>(const CsumArgs &, hipStream_t);
+extern template int launch_txrows<true>(const CsumArgs &, hipStream_t);
 // k_stash.hip: the class kernel's stash modes on one-wave workgroups
 int launch_fill(const CsumArgs &a, dim3 grid, hipStream_t st);
 int launch_rx(const CsumArgs &a, dim3 grid, hipStream_t st);

@@ -365,9 +365,11 @@ def test_chains(oracle, win, hint, runs):
     assert diff.size == 0, [(int(i), int(got[i]), int(want[i])) for i in diff[:5]]
 
 
-def test_chain_fill(oracle, win):
+@pytest.mark.parametrize("txp", [False, True])
+def test_chain_fill(oracle, win, txp):
     """Head-fragment fill (rns_csum_chain_fill_dev): the chain folded like util.rs:112-119
-    with the field counted as zero, stored big-endian into the head fragment."""
+    with the field counted as zero, stored big-endian into the head fragment (txp: the
+    transmit-rows kernel's exact loop, these chains being scattered)."""
     off, mini_off, ln, first = chain_windows(win, 1500, 7, 600, min_head=20)  # heads hold a 20-byte header
     n = first.size - 1
     seeds = (O.splitmix64_words(0xCC, n) & np.uint64(0xFFFF)).astype(np.uint16)
@@ -383,7 +385,7 @@ def test_chain_fill(oracle, win):
     out = torch.empty(n, dtype=torch.uint16, device=DEV)
     try:
         csum_chain_fill(win.arena, dev(off, np.int64), dev(ln, np.int32), dev(first, np.int32), dev(seeds, np.int16),
-                        field=dev(field, np.int16), out=out, frag_len_hint=512)
+                        field=dev(field, np.int16), out=out, frag_len_hint=512, tx_packed=txp)
         assert np.array_equal(host_u16(out), want)
         got = np.concatenate(win.snapshot())
         diff = np.flatnonzero(got != want_arena)

@@ -45,6 +45,10 @@ def expected(oracle, arena, off, ln, first, seeds, field, complement=True):
     head = np.where(ok_range, f0, 0)
     hl = ln[head].astype(np.int64) if nf else np.zeros(f0.size, dtype=np.int64)
     fits = ok_range & (field.astype(np.int64) + 2 <= hl)
+    # a fragment outside the arena rejects its packet
+    frag_out = (off.astype(np.int64) + ln.astype(np.int64)) > arena.size
+    cb = np.concatenate([[0], np.cumsum(frag_out)])
+    fits &= ~(ok_range & (cb[np.minimum(f1, nf)] - cb[np.minimum(f0, nf)] > 0))
     idx = off[head].astype(np.int64) + field.astype(np.int64)
     a[idx[fits]] = 0
     a[idx[fits] + 1] = 0
@@ -60,7 +64,8 @@ def expected(oracle, arena, off, ln, first, seeds, field, complement=True):
     return want, fits, a
 
 
-def run_fill(arena_np, off, ln, first, seeds, field, *, hint=512, runs=False, per_packet=True, complement=True):
+def run_fill(arena_np, off, ln, first, seeds, field, *, hint=512, runs=False, per_packet=True, complement=True,
+             tx_packed=False):
     a = torch.from_numpy(arena_np.copy()).to(DEV)
     n = first.size - 1
     out = torch.empty(n, dtype=torch.uint16, device=DEV)
@@ -70,7 +75,7 @@ def run_fill(arena_np, off, ln, first, seeds, field, *, hint=512, runs=False, pe
                     None if seeds is None else dev(np.asarray(seeds, np.uint16), np.int16),
                     field=dev(np.asarray(field, np.uint16), np.int16) if per_packet else None,
                     field_off=int(field[0]) if n else 16, complement=complement, out=out, bad=bad,
-                    frag_len_hint=hint, runs=runs)
+                    frag_len_hint=hint, runs=runs, tx_packed=tx_packed)
     return host_u16(out), int(bad.item()), a.cpu().numpy()
 
 
@@ -101,14 +106,15 @@ def test_tcp_output_shape_kat(oracle):
     assert fits.all()
 
 
-@pytest.mark.parametrize("hint,runs", [(512, False), (100, False), (512, True), (40, True)])
-def test_random_transmit_chains(oracle, hint, runs):
+@pytest.mark.parametrize("hint,runs,txp", [(512, False, False), (100, False, False), (512, True, False),
+                                           (40, True, False), (512, False, True)])
+def test_random_transmit_chains(oracle, hint, runs, txp):
     """Heads of 4-60 bytes back to back in a header region (any start parity), payloads of
     0-5 fragments (odd non-final lengths, empty fragments, back-to-back runs and scattered
     pieces), per-packet fields 2 / 6 / 16 / odd, seeds, rejects (no fragments, heads too
     short for the field)."""
     n = 30_000
-    w = O.splitmix64_words(0xCF11 + hint + runs, 4 * n)
+    w = O.splitmix64_words(0xCF11 + hint + runs + 2 * txp, 4 * n)
     hl = (w[:n] % np.uint64(57)).astype(np.int64) + 4
     npay = (w[n:2 * n] % np.uint64(6)).astype(np.int64)
     npay[::97] = -1                                         # no fragments at all: rejected
@@ -136,8 +142,99 @@ def test_random_transmit_chains(oracle, hint, runs):
                 pos += L
         first.append(len(off))
     arena = O.splitmix64_bytes(0xCF13 + hint, pos + 64)
+    # (with the transmit hint these scattered chains take the exact per-packet loop)
     check(oracle, arena, np.array(off), np.array(ln), np.array(first, dtype=np.uint32), seeds, field, hint=hint,
-          runs=runs)
+          runs=runs, tx_packed=txp)
+
+
+def tx_blocks(n_blocks, salt):
+    """64-packet blocks in the transmit shape RNS_FLAG_CHAIN_TX_PACKED names: heads of 1..64
+    bytes back to back in a header region ((start & 15) + length <= 64), then payload runs of
+    0-4 pieces (even non-final lengths, empty pieces included) at 16-byte starts with gaps of
+    0-3 chunks; some packets rejected (field past the head, no fragments, a piece outside the
+    arena).  Every 5th block is broken on purpose (a 70-byte head, an unaligned payload, a
+    descending payload, an odd non-final piece, 5 pieces, a 400 KB gap): the exact loop."""
+    n = 64 * n_blocks
+    w = O.splitmix64_words(0xCF60 + salt, 8 * n)
+    field = np.array([16, 6, 2, 3, 17], dtype=np.uint16)[(w[:n] % np.uint64(5)).astype(np.int64)]
+    heads, hpos = [], 5
+    for i in range(n):
+        room = 64 - (hpos & 15)
+        hl = 1 + int(w[n + i] % np.uint64(room))
+        hl = max(hl, min(room, int(field[i]) + 2)) if i % 11 else hl
+        heads.append((hpos, hl))
+        hpos += hl
+    spare = hpos + 64                                       # own room for the 70-byte heads
+    ppos = (hpos + 4096 + 15) & ~15
+    off, ln, first = [], [], [0]
+    late = []
+    for i in range(n):
+        b, lane = divmod(i, 64)
+        brk = (b // 5) % 6 if b % 5 == 4 else -1
+        if i % 97 == 13:                                    # no fragments: rejected
+            first.append(len(off))
+            continue
+        h0, hl = heads[i]
+        if brk == 0 and lane == 9:                          # (not overlapping the other heads)
+            h0, hl, spare = spare, 70, spare + 80
+        off.append(h0)
+        ln.append(hl)
+        plen = int(w[2 * n + i] % np.uint64(3000)) if i % 7 else 0
+        npc = 1 + int(w[3 * n + i] % np.uint64(4)) if plen else int(i % 14 == 0)
+        if brk == 4 and lane == 20:
+            npc, plen = 5, max(plen, 100)
+        cuts = sorted(int(x) & ~1 for x in (w[4 * n + i] % np.uint64(plen + 1), w[5 * n + i] % np.uint64(plen + 1),
+                                              w[6 * n + i] % np.uint64(plen + 1), w[7 * n + i] % np.uint64(plen + 1)))
+        cuts = [0] + cuts[:npc - 1] + [plen] if npc else []
+        ppos += 16 * int(w[4 * n + i] % np.uint64(4))
+        if brk == 1 and lane == 30:
+            ppos += 8
+        if brk == 5 and lane == 40:
+            ppos += 400_000
+        start = ppos
+        if brk == 2 and lane == 5:
+            late.append(i)
+            start = (24 << 20) + 4096 * len(late)           # this payload lies after every other one
+        for k in range(npc):
+            L = cuts[k + 1] - cuts[k]
+            if brk == 3 and lane == 50 and k == 0 and npc > 1:
+                L += 1                                      # odd non-final piece: not a run
+            off.append(start + cuts[k] + (1 if brk == 3 and lane == 50 and k > 0 and npc > 1 else 0))
+            ln.append(max(L, 0))
+        if start == ppos:
+            ppos = (ppos + plen + 1 + 15) & ~15
+        if i % 89 == 60 and npc:                            # a piece outside the arena: rejected
+            off[-1] = 1 << 40
+        first.append(len(off))
+    end = max(ppos, max(o + l for o, l in zip(off, ln) if o < (1 << 40))) + 256
+    arena = O.splitmix64_bytes(0xCF61 + salt, end)
+    seeds = (w[:n] >> np.uint64(24) & np.uint64(0xFFFF)).astype(np.uint16)
+    return arena, np.array(off, dtype=np.uint64), np.array(ln, dtype=np.uint32), np.array(first, np.uint32), \
+        seeds, field
+
+
+@pytest.mark.parametrize("hint", [512, 100])
+def test_tx_packed_blocks(oracle, hint):
+    """RNS_FLAG_CHAIN_TX_PACKED on tx_blocks: the fill, every result and every arena byte
+    against the oracle; the plain chain checksum of the same chains with the hint == the
+    oracle (and == without it)."""
+    arena, off, ln, first, seeds, field = tx_blocks(60, hint)
+    check(oracle, arena, off, ln, first, seeds, field, hint=hint, tx_packed=True)
+    a = torch.from_numpy(arena).to(DEV)
+    args = (a, dev(off, np.int64), dev(ln, np.int32), dev(first, np.int32), dev(seeds, np.int16))
+    plain = host_u16(csum_chain(*args, complement=True, frag_len_hint=hint))
+    txp = host_u16(csum_chain(*args, complement=True, frag_len_hint=hint, tx_packed=True))
+    assert np.array_equal(txp, plain)
+    inside = np.array([all(int(o) + int(L) <= arena.size for o, L in zip(off[first[i]:first[i + 1]],
+                                                                       ln[first[i]:first[i + 1]]))
+                       for i in range(first.size - 1)])
+    keep = inside & (first[1:] > first[:-1])
+    sel = np.flatnonzero(keep)
+    cnt = (first[1:] - first[:-1])[sel].astype(np.int64)
+    nf = np.concatenate([[0], np.cumsum(cnt)])
+    fr = np.repeat(first[:-1][sel].astype(np.int64), cnt) + (np.arange(int(nf[-1])) - np.repeat(nf[:-1], cnt))
+    ref = oracle.chain_batch(arena, off[fr], ln[fr], nf.astype(np.uint32), seeds[sel], complement=True)
+    assert np.array_equal(txp[sel], ref)
 
 
 @pytest.mark.parametrize("hint", [512, 100])
@@ -256,12 +353,13 @@ def test_full_size_transmit_chains(oracle, name, frag):
     f_s = int(lay.first[sample])
     host_before = a[:int(lay.frag_off[f_s - 1] + lay.frag_len[f_s - 1]) + 64].cpu().numpy() \
         if name == "c3_1500B" else None
-    for runs in (False, True):
+    for runs, txp in ((False, False), (True, False), (False, True)):
         out = torch.empty(lay.n, dtype=torch.uint16, device=DEV)
         bad = torch.zeros(1, dtype=torch.int32, device=DEV)
-        csum_chain_fill(a, d_off, d_len, d_first, d_seed, field_off=lay.field, out=out, bad=bad, runs=runs)
+        csum_chain_fill(a, d_off, d_len, d_first, d_seed, field_off=lay.field, out=out, bad=bad, runs=runs,
+                        tx_packed=txp)
         assert int(bad.item()) == 0
-        rx = host_u16(csum_chain(a, d_off, d_len, d_first, d_seed, complement=True, runs=runs))
+        rx = host_u16(csum_chain(a, d_off, d_len, d_first, d_seed, complement=True, runs=runs, tx_packed=txp))
         assert not rx.any()
         if host_before is not None and not runs:
             want, _, _ = expected(oracle, host_before, lay.frag_off[:f_s], lay.frag_len[:f_s],

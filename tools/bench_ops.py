@@ -200,14 +200,14 @@ def bench_chain_fill(cfg, dev, args, frag):
     hint = int(round(pay / nf))
     tag = "tx" if frag == 0 else f"tx{frag}"
     res = {}
-    for runs in (False, True):
-        sfx = "_runs" if runs else ""
+    for runs, txp in ((False, False), (True, False), (False, True)):
+        sfx = "_runs" if runs else "_txpacked" if txp else ""
         ms = timed(lambda: csum_chain_fill(arena, d_fo, d_fl, d_first, seed, field_off=t.field, out=out,
-                                           frag_len_hint=hint, runs=runs), args.steps, args.rounds)
+                                           frag_len_hint=hint, runs=runs, tx_packed=txp), args.steps, args.rounds)
         res[f"chain_fill_{tag}{sfx}"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1),
                                         "fragments": nf, "hint": hint}
         ms = timed(lambda: csum_chain(arena, d_fo, d_fl, d_first, seed, complement=True, out=out,
-                                      frag_len_hint=hint, runs=runs), args.steps, args.rounds)
+                                      frag_len_hint=hint, runs=runs, tx_packed=txp), args.steps, args.rounds)
         res[f"chain_{tag}{sfx}"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1)}
     del arena
     torch.cuda.empty_cache()
