@@ -21,8 +21,15 @@ int launch_stream_rx(const CsumArgs &a, hipStream_t st)
 {
     const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);
     constexpr bool NT = RNS_STREAM_NT != 0;
+    // ACK-sized datagrams (at most 128 arena bytes per datagram): the instantiation without the rows
+    const bool ack = a.arena_bytes / a.n <= 128;
     if (RNS_RX_ROWS) {
-        if (buf_records(a) < kOobOffset)
+        const bool buf = buf_records(a) < kOobOffset;
+        if (ack && buf)
+            hipLaunchKernelGGL((csum_rows_rx_kernel<NT, true, RNS_RX_ROWS_D, true>), grid, block, 0, st, a);
+        else if (ack)
+            hipLaunchKernelGGL((csum_rows_rx_kernel<NT, false, RNS_RX_ROWS_D, true>), grid, block, 0, st, a);
+        else if (buf)
             hipLaunchKernelGGL((csum_rows_rx_kernel<NT, true, RNS_RX_ROWS_D>), grid, block, 0, st, a);
         else
             hipLaunchKernelGGL((csum_rows_rx_kernel<NT, false, RNS_RX_ROWS_D>), grid, block, 0, st, a);

@@ -146,7 +146,8 @@ def test_two_rank_gloo_bench_main(tmp_path, oracle, config, n, launch):
         assert per_rank == [n, n]
         step_bytes = 2 * whole
     assert abs(line["value"] - step_bytes * 3 / (line["ms_per_step"] * 3e-3) / 2 ** 30) <= 0.02 * line["value"] + 0.01
-    # the gathered results on EVERY rank are the oracle's for every rank's packets, in rank order
+    # the gathered results on EVERY rank (left by the last leg, the overlapped one) are the
+    # oracle's for every rank's packets, in rank order
     expect = []
     for rank in (0, 1):
         if strong:

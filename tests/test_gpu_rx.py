@@ -186,7 +186,7 @@ def test_tiny_datagrams_capped_grid_every_status():
     assert np.array_equal(st, want)
 
 
-# --- packed receive arenas (rns_rx_verify_packed_dev: the stream kernel) ---------------
+# --- packed receive arenas (rns_rx_verify_packed_dev: the rows receive kernel) ---------
 def run_packed_rx(pkts, align_log2, first_off, base_shift=0):
     from rustnetworkstack_amd.batch import packed_layout, rx_verify_packed
     ln = np.array([len(p) for p in pkts], dtype=np.uint32)
@@ -233,6 +233,33 @@ def test_packed_edge_datagrams_match_reference_path(oracle):
         got = list(zip(st.tolist(), l4.tolist()))
         bad = [(i, len(pkts[i]), got[i], expect[i]) for i in range(len(pkts)) if got[i] != tuple(expect[i])]
         assert not bad, (first_off, bad[:5])
+
+
+def test_packed_ack_arena_with_longer_datagrams(oracle):
+    """An arena of ACK-sized datagrams (at most 128 arena bytes per datagram: the receive
+    kernel's instantiation without the rows) in which a few units hold longer datagrams
+    (every 37th unit one of 1400 B, one of 65): those units take the per-datagram wave loop;
+    every status and L4 sum against the reference's receive path."""
+    n = 64 * 300
+    w = O.splitmix64_words(0xAC4, n)
+    pkts = []
+    for i in range(n):
+        size = int(w[i] % np.uint64(25))
+        p = bytearray(ipv4(6, tcp_seg(R4, L4, bytes([i & 0xFF]) * size)))
+        if (i // 64) % 37 == 3 and i % 64 == 17:
+            p = bytearray(ipv4(6, tcp_seg(R4, L4, O.splitmix64_bytes(i, 1360).tobytes())))
+        if (i // 64) % 37 == 5 and i % 64 == 40:
+            p = bytearray(ipv6(58, tcp_seg(R6, L6, b"\x11" * 21, proto=58, field=2, hlen=4)))
+        if (w[i] >> np.uint64(32)) % np.uint64(11) == 0:
+            p[int(w[i] >> np.uint64(8)) % len(p)] ^= 0x10
+        pkts.append(bytes(p))
+    ln = np.array([len(p) for p in pkts])
+    assert ((ln + 15) // 16 * 16).sum() // n <= 128 and ln.max() > 64
+    expect = [O.rx_verify_ref(p, L4, L6, ones_comp=oracle.compute_ones_comp) for p in pkts]
+    st, l4 = run_packed_rx(pkts, 4, 0)
+    got = list(zip(st.tolist(), l4.tolist()))
+    bad = [(i, len(pkts[i]), got[i], expect[i]) for i in range(len(pkts)) if got[i] != tuple(expect[i])]
+    assert not bad, bad[:5]
 
 
 @pytest.mark.parametrize("name", ["c2_64B", "c5_imix"])
