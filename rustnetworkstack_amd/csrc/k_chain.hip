@@ -10,6 +10,12 @@ int launch_chain(const CsumArgs &a, uint32_t K, bool nt, bool runs, hipStream_t 
     const uint64_t waves = (static_cast<uint64_t>(a.n) + 64 * K - 1) / (64 * K);
     const dim3 grid(static_cast<uint32_t>((waves + kChainBlock / 64 - 1) / (kChainBlock / 64))), block(kChainBlock);
     const bool buf = buf_records(a) < kOobOffset;
+    // The temporal plain checksum (IMIX-like fragments) at 4 waves/SIMD for chains of 3+ packets
+    // per lane or 2+ fragments per packet (IMIX [492, 512, rest] chains 640 -> 598 us, IMIX
+    // transmit chains in 512-byte fragments 900 -> 790), else at 3 (IMIX in 512-byte NetBuffers
+    // 811 -> 754, [head, payload] chains 658 -> 620; session r05f, both forms free of scratch).
+    const double mean = static_cast<double>(a.n_frags) / static_cast<double>(a.n);
+    const bool deep = !FILL && (K >= 3 || (K == 2 && mean >= 2.0));
 #define RNS_CHAIN_LAUNCH(KM)                                                                      \
     if (runs && nt)                                                                               \
         hipLaunchKernelGGL((csum_chain_kernel<true, true, KM, true, FILL>), grid, block, 0, st, a);  \
@@ -19,6 +25,8 @@ int launch_chain(const CsumArgs &a, uint32_t K, bool nt, bool runs, hipStream_t 
         hipLaunchKernelGGL((csum_chain_kernel<true, true, KM, false, FILL>), grid, block, 0, st, a); \
     else if (nt)                                                                                  \
         hipLaunchKernelGGL((csum_chain_kernel<true, false, KM, false, FILL>), grid, block, 0, st, a); \
+    else if (buf && deep)                                                                         \
+        hipLaunchKernelGGL((csum_chain_kernel<false, true, KM, false, FILL, FILL ? 0 : 4>), grid, block, 0, st, a); \
     else if (buf)                                                                                 \
         hipLaunchKernelGGL((csum_chain_kernel<false, true, KM, false, FILL>), grid, block, 0, st, a); \
     else                                                                                          \

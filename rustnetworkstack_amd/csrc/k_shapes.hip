@@ -114,4 +114,19 @@ int dispatch(const CsumArgs &a, uint32_t variant, uint32_t G, uint32_t U, uint32
 template int dispatch<false>(const CsumArgs &, uint32_t, uint32_t, uint32_t, uint32_t, hipStream_t);
 template int dispatch<true>(const CsumArgs &, uint32_t, uint32_t, uint32_t, uint32_t, hipStream_t);
 
+// Tiny fixed-size packets at a fixed 16-byte-aligned stride: csum_strided_tiny_kernel.
+#ifndef RNS_STRIDED_TINY_B  // 64-packet batches per wave
+#define RNS_STRIDED_TINY_B 1
+#endif
+int launch_strided_tiny(const CsumArgs &a, hipStream_t st)
+{
+    constexpr int B = RNS_STRIDED_TINY_B;
+    const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 64 * B - 1) / (64 * B))), block(64);
+    if (buf_records(a) < kOobOffset)
+        hipLaunchKernelGGL((csum_strided_tiny_kernel<true, B>), grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL((csum_strided_tiny_kernel<false, B>), grid, block, 0, st, a);
+    return hip_status(hipGetLastError());
+}
+
 }  // namespace rns

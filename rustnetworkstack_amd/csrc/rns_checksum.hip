@@ -202,6 +202,12 @@ int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uin
     a.fixed_len = len;
     a.n = n;
     a.flags = flags;
+#ifndef RNS_STRIDED_TINY  // A/B knob (round 5): 0 = tiny strided packets through the rounds kernel
+#define RNS_STRIDED_TINY 1
+#endif
+    // packets of at most 64 bytes at 16-byte-aligned starts: the strided tiny kernel (c2)
+    if (RNS_STRIDED_TINY && len != 0 && len <= 64 && ((first_off + a.base_adjust) & 15) == 0 && (stride & 15) == 0)
+        return launch_strided_tiny(a, static_cast<hipStream_t>(stream));
     const Shape sh = pick_shape(len);
     return dispatch<true>(a, sh.variant, sh.G, sh.U, sh.max_blocks, static_cast<hipStream_t>(stream));
 }

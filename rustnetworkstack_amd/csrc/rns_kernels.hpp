@@ -1596,21 +1596,27 @@ csum_mixed_kernel(const CsumArgs a)
 // instantiation spills 8-44 B/lane (8 on the default path); 3 waves/SIMD spills nothing
 // and is 4-7 % slower on c3 chains (session r04b), so 4 stays (tools/scratch_report.sh).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
+// Inclusive max over the 64 lanes (Hillis-Steele over DPP row shifts, then the row broadcasts).
+// DPP, not __shfl_xor: the shuffles' lane-address registers are loop invariants the compiler
+// hoisted and then spilled in the chain kernel (round 5).
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v)
 {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1)
-        v = min(v, static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), m, 64)));
-    return __builtin_amdgcn_readfirstlane(v);
+    uint32_t x = v;
+    x = max(x, dpp_or_zero<0x111>(x));           // row_shr:1
+    x = max(x, dpp_or_zero<0x112>(x));           // row_shr:2
+    x = max(x, dpp_or_zero<0x114>(x));           // row_shr:4
+    x = max(x, dpp_or_zero<0x118>(x));           // row_shr:8
+    x = max(x, dpp_or_zero<0x142, 0xA, 0xF>(x));  // row_bcast:15 into rows 1 and 3
+    x = max(x, dpp_or_zero<0x143, 0xC, 0xF>(x));  // row_bcast:31 into rows 2 and 3
+    return x;
 }
 
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
 {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1)
-        v = max(v, static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), m, 64)));
-    return __builtin_amdgcn_readfirstlane(v);
+    return __builtin_amdgcn_readlane(wave_incl_max(v), 63);
 }
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) { return ~wave_max_u32(~v); }
 
 constexpr uint32_t kChainMaxK = 8;  // packets per lane, at most
 
@@ -1676,43 +1682,30 @@ __device__ __forceinline__ uint32_t fragment_run(const CsumArgs &a, uint32_t f0,
     return run && tot <= kNoWrapBytes ? tot : kNoRun;
 }
 
-// Waves/SIMD of the chain kernel: 4 (128 VGPRs) where the instantiation fits them with no
-// scratch — the nontemporal buffer forms of the plain checksum (NetBuffer-sized fragments: c3
-// chains 4-7 % faster than at 3, session r04b) — and 3 (168 VGPRs) for the rest, which spill
-// 8-52 B/lane at 4 (the temporal class pass with its tiny class, the 64-bit addresses of
-// arenas of 4 GiB and more, the fill's extra state; profiles/r05_resources.txt).
-// -DRNS_CHAIN_OCC=n forces n for every instantiation (A/B builds).
-template <bool NT, bool BUF, uint32_t KMAX, bool RUNS, bool FILL>
+// Waves/SIMD of the chain kernel (every instantiation free of scratch: tools/scratch_report.sh,
+// profiles/r05_resources.txt): 4 (128 VGPRs) for the nontemporal buffer forms — NetBuffer-sized
+// fragments, c3 chains 4-7 % faster than at 3 (session r04b) — and 3 (168 VGPRs) for the rest:
+// at 4 the temporal runs / fill forms and the 64-bit addresses of arenas of 4 GiB and more
+// spill 8-20 B/lane.  The temporal plain checksum (IMIX-like fragments) fits 4 without scratch
+// too and has both: the launcher picks by the chain shape (OCC below).  -DRNS_CHAIN_OCC=n
+// forces n for every instantiation (A/B builds).
+template <bool NT, bool BUF, uint32_t KMAX, bool RUNS, bool FILL, int OCC>
 constexpr int chain_occ()
 {
 #ifdef RNS_CHAIN_OCC
     return RNS_CHAIN_OCC;
 #else
-    return (NT && BUF && !FILL && !(RUNS && KMAX > 1)) ? 4 : 3;
+    return OCC ? OCC : (NT && BUF) ? 4 : 3;
 #endif
 }
 // Workgroup size of the chain kernel: one wave.  Its per-packet state is LDS, which is
 // freed per workgroup, as for the mixed kernel's stash modes: IMIX chains 640 -> 608 us
 // packed, 839 -> 771 us in 512-byte buffers, c3 equal (profiles/r02_block_ab.json).
-#ifndef RNS_CHAIN_BLOCK
-#define RNS_CHAIN_BLOCK 64
-#endif
-constexpr int kChainBlock = RNS_CHAIN_BLOCK;
+constexpr int kChainBlock = 64;
 // RUNS: the RNS_FLAG_CHAIN_RUNS instantiation (buffer path only).  A separate kernel:
 // compiled into the plain one, the run check cost it ~5 % (registers) even unused.
-//
-// FILL (rns_csum_chain_fill_dev, the transmit shape of tcp_output / udp_output /
-// icmp_output_*: tcp.rs:957-973, udp.rs:158-171, icmp.rs:87-112): the packet's checksum
-// field lies in its FIRST fragment (the head fragment alloc_header prepended, buf.rs:262-
-// 291), counts as zero (buf.rs:286-288), and receives the result big-endian (set_be16,
-// the header_mut() slice = the first fragment).  The owner loads the field's two bytes
-// with its descriptors and takes their contribution out of the head fragment's EXACT word
-// sum before it is folded (the lane that summed the fragment hands the raw sum over), so
-// zero sums fold exactly as the reference's; after the fold it stores the two bytes.  A
-// packet whose head fragment cannot hold its field (or has no fragments) is rejected:
-// result 0, counted, nothing stored.
-template <bool NT, bool BUF, uint32_t KMAX, bool RUNS = false, bool FILL = false>
-__global__ __launch_bounds__(kChainBlock, (chain_occ<NT, BUF, KMAX, RUNS, FILL>())) void csum_chain_kernel(const CsumArgs a)
+template <bool NT, bool BUF, uint32_t KMAX, bool RUNS = false, bool FILL = false, int OCC = 0>
+__global__ __launch_bounds__(kChainBlock, (chain_occ<NT, BUF, KMAX, RUNS, FILL, OCC>())) void csum_chain_kernel(const CsumArgs a)
 {
     static_assert(!RUNS || BUF, "runs: buffer path only");
     // A wave owns K*64 consecutive packets (K = a.chain_k, chosen by the host from the
@@ -2571,6 +2564,80 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : FILL ? RNS_ROWS_FILL_OCC : 8) voi
 }
 
 // ---------------------------------------------------------------------------
+// Tiny fixed-size packets at a fixed stride (rns_csum_batch_strided_dev, c2: 2^20 x 64 B):
+// packet i = arena[first_off + i * stride, + len) with len <= 64 and 16-byte-aligned starts,
+// so a packet is at most 4 chunks and a wave's 64 packets are 4 rows of 16 packets x 4 chunks
+// whose addresses the lanes compute themselves — no descriptors but the seeds, no per-round
+// broadcast (the rounds kernel's fetch_pkt), every row of every batch in flight at once.  A
+// quad of lanes sums its packet (two DPP steps); the owner lane pulls its packet's sum with one
+// ds_bpermute per row and finishes (util.rs:88-106: the LE sum folded and byte-swapped — the
+// starts are even — plus the seed, folded).
+// ---------------------------------------------------------------------------
+template <bool BUF, int B>
+__global__ __launch_bounds__(64) void csum_strided_tiny_kernel(const CsumArgs a)
+{
+    const uint32_t lane = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
+    const uint64_t recs = buf_records(a);
+    const uint32_t L = a.fixed_len;  // 1..64
+    const uint32_t j = lane & 3u;
+    const uint32_t jb = 16u * j;
+    const uint64_t start0 = a.first_off + a.base_adjust;
+    uint4 v[B][4];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const uint64_t base = (static_cast<uint64_t>(blockIdx.x) * B + b) * 64;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint64_t q = base + 16u * r + (lane >> 2);
+            const uint64_t o = start0 + q * a.stride + jb;
+            const bool in = q < a.n && jb < L && o + 16 <= recs;
+            if constexpr (BUF) {
+                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, in ? static_cast<uint32_t>(o) : kOobOffset, 0,
+                                                                      kNtAux);
+                v[b][r] = make_uint4(x.x, x.y, x.z, x.w);
+            } else {
+                const uint4 x = load_chunk<true>(a.arena + (in ? o : 0));
+                v[b][r] = in ? x : make_uint4(0, 0, 0, 0);
+            }
+        }
+    }
+    const int src = static_cast<int>((lane & 15u) << 4);  // lane 4 * (p & 15) of the owner's row
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const uint64_t base = (static_cast<uint64_t>(blockIdx.x) * B + b) * 64;
+        const uint64_t p = base + lane;
+        uint32_t mine = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            uint4 x = v[b][r];
+            if (jb + 16u > L)  // the packet's last chunk: its bytes past len never count
+                x = jb < L ? keep_first(x, L - jb) : make_uint4(0, 0, 0, 0);
+            uint32_t t = __builtin_amdgcn_sad_u16(x.x, 0, 0u);
+            t = __builtin_amdgcn_sad_u16(x.y, 0, t);
+            t = __builtin_amdgcn_sad_u16(x.z, 0, t);
+            t = __builtin_amdgcn_sad_u16(x.w, 0, t);
+            t = group_allreduce<4>(t);
+            const uint32_t got = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(t)));
+            mine = (lane >> 4) == static_cast<uint32_t>(r) ? got : mine;
+        }
+        if (p < a.n) {
+            const uint64_t st = start0 + p * a.stride;
+            const bool ok = st <= a.arena_bytes && L <= a.arena_bytes - st;
+            const uint32_t sd = a.seed ? static_cast<uint32_t>(a.seed[p]) : 0u;
+            a.out[p] = finalize_bits(mine, false, false, sd, ok, a.flags);  // 64 consecutive u16: one 128-byte store
+        }
+        if (a.bad) {
+            const uint64_t st = start0 + p * a.stride;
+            const uint64_t rejected = __ballot(p < a.n && !(st <= a.arena_bytes && L <= a.arena_bytes - st));
+            if (rejected && lane == 0)
+                atomicAdd(a.bad, static_cast<uint32_t>(__popcll(rejected)));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Receive verify through the rows decomposition (rns_rx_verify_packed_dev, round 5):
 // ip_input_v4 (ip.rs:65-92), ip_input_v6 (ip.rs:114-121), tcp::validate_checksum
 // (tcp.rs:838-850), icmp_input_v4/v6 (icmp.rs:44-75) over a packed arena of datagrams.  The
@@ -2621,8 +2688,24 @@ __global__ __launch_bounds__(64, ACK ? RNS_RX_ACK_OCC : RNS_ROWS_RX_OCC) void cs
     uint32_t mine = 0;
     uint4 own[kNS + 1];
     own[kNS] = make_uint4(0, 0, 0, 0);
-    uint32_t s0 = 0;
-    bool odd = false;
+    // the owner's finish (rx_finish), called in each path with that path's start offset and
+    // parity: constants on the aligned paths, so their finish keeps only the aligned code
+    auto finish = [&](uint32_t s0, bool odd) {
+        uint32_t l4_res = 0;
+        const uint8_t stv = rx_finish<kNS + 1>(a, own, mine, s0, len, odd, false, live && ok && len != 0, l4_res);
+        if (live) {
+            a.status[p] = stv;
+            if (a.l4_out)
+                a.l4_out[p] = static_cast<uint16_t>(l4_res);
+        }
+    };
+#ifdef RNS_RX_ACK_LDS  // A/B experiment: reserve LDS per workgroup in the ACK instantiation
+    if constexpr (ACK) {
+        __shared__ uint4 pad_lds[RNS_RX_ACK_LDS / 16];
+        if (a.n == 0xFFFFFFFFu)
+            pad_lds[lane] = make_uint4(lane, 0, 0, 0);
+    }
+#endif
     if ((r0 & 15) == 0 && !__ballot(len > 64)) {
         // ---- ACK-sized unit: every owner takes its datagram whole ----
 #pragma unroll
@@ -2639,6 +2722,7 @@ __global__ __launch_bounds__(64, ACK ? RNS_RX_ACK_OCC : RNS_ROWS_RX_OCC) void cs
             mine = __builtin_amdgcn_sad_u16(x.z, 0, mine);
             mine = __builtin_amdgcn_sad_u16(x.w, 0, mine);
         }
+        finish(0u, false);
     } else if (!ACK && (r0 & 15) == 0) {
         // ---- the rows: T, and the owner's first 4 chunks loaded a group ahead ----
         const uint32_t c0 = excl >> 4;
@@ -2648,6 +2732,7 @@ __global__ __launch_bounds__(64, ACK ? RNS_RX_ACK_OCC : RNS_ROWS_RX_OCC) void cs
         for (int i = 0; i < kNS; ++i)  // zeros past the datagram's end (the region's next bytes)
             if (16u * i + 16u > len)
                 own[i] = 16u * i < len ? keep_first(own[i], len - 16u * i) : make_uint4(0, 0, 0, 0);
+        finish(0u, false);
     } else {
         // ---- unaligned region (rare; ACK: a unit with a longer datagram): the whole wave sums
         // one datagram at a time ----
@@ -2671,11 +2756,10 @@ __global__ __launch_bounds__(64, ACK ? RNS_RX_ACK_OCC : RNS_ROWS_RX_OCC) void cs
             const uint32_t sum = group_allreduce<64>(acc);
             mine = lane == o ? sum : mine;
         }
-        odd = r0 & 1;  // every datagram of the range shares the region start's misalignment
         // each owner takes its header from the 16-byte boundary below its start: 5 chunks hold
         // its first 65-80 bytes, masked to the datagram
         const uint64_t b0 = start & ~15ull;
-        s0 = static_cast<uint32_t>(start & 15);
+        const uint32_t s0 = static_cast<uint32_t>(start & 15);
 #pragma unroll
         for (int i = 0; i < kNS + 1; ++i)
             own[i] = own_chunk<BUF>(a, rsrc, recs, b0, (len && ok) ? s0 + len : 0u, i);
@@ -2685,13 +2769,7 @@ __global__ __launch_bounds__(64, ACK ? RNS_RX_ACK_OCC : RNS_ROWS_RX_OCC) void cs
             own[i] = make_uint4(keep_bytes(own[i].x, lo, hi, 0), keep_bytes(own[i].y, lo, hi, 4),
                                 keep_bytes(own[i].z, lo, hi, 8), keep_bytes(own[i].w, lo, hi, 12));
         }
-    }
-    uint32_t l4_res = 0;
-    const uint8_t stv = rx_finish<kNS + 1>(a, own, mine, s0, len, odd, false, live && ok && len != 0, l4_res);
-    if (live) {
-        a.status[p] = stv;
-        if (a.l4_out)
-            a.l4_out[p] = static_cast<uint16_t>(l4_res);
+        finish(s0, r0 & 1);  // every datagram of the range shares the region start's misalignment
     }
 }
 
@@ -2723,19 +2801,6 @@ __global__ __launch_bounds__(64, ACK ? RNS_RX_ACK_OCC : RNS_ROWS_RX_OCC) void cs
 #define RNS_TXROWS_OCC 5  // (zero scratch at 86-89 VGPRs; 6 spills 32-116 B/lane)
 #endif
 constexpr uint32_t kTxHeadMax = 64;  // (head start & 15) + head length: at most 4 chunks
-
-// Inclusive max over the 64 lanes (Hillis-Steele over DPP row shifts, then the row broadcasts).
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v)
-{
-    uint32_t x = v;
-    x = max(x, dpp_or_zero<0x111>(x));           // row_shr:1
-    x = max(x, dpp_or_zero<0x112>(x));           // row_shr:2
-    x = max(x, dpp_or_zero<0x114>(x));           // row_shr:4
-    x = max(x, dpp_or_zero<0x118>(x));           // row_shr:8
-    x = max(x, dpp_or_zero<0x142, 0xA, 0xF>(x));  // row_bcast:15 into rows 1 and 3
-    x = max(x, dpp_or_zero<0x143, 0xC, 0xF>(x));  // row_bcast:31 into rows 2 and 3
-    return x;
-}
 
 __device__ __forceinline__ uint32_t bswap16_u32(uint32_t x) { return ((x & 0xff) << 8) | (x >> 8); }
 

@@ -70,6 +70,7 @@ template <bool S>
 int dispatch(const CsumArgs &a, uint32_t variant, uint32_t G, uint32_t U, uint32_t max_blocks, hipStream_t st);
 extern template int dispatch<false>(const CsumArgs &, uint32_t, uint32_t, uint32_t, uint32_t, hipStream_t);
 extern template int dispatch<true>(const CsumArgs &, uint32_t, uint32_t, uint32_t, uint32_t, hipStream_t);
+int launch_strided_tiny(const CsumArgs &a, hipStream_t st);
 // k_packed.hip
 int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st);
 int launch_fill_packed(const CsumArgs &a, hipStream_t st);

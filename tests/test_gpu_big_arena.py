@@ -144,9 +144,12 @@ def test_packed_checksum(oracle, win, kind, hint, align_log2):
     assert int(bad.item()) == 0
 
 
-def test_strided_across_the_line(oracle, win):
-    n, stride, L = 20_000, 80, 64
-    first = FOUR_G - 64 * 10_000 - 3
+@pytest.mark.parametrize("first_adj,stride,L", [(-3, 80, 64), (0, 64, 64), (0, 48, 40)])
+def test_strided_across_the_line(oracle, win, first_adj, stride, L):
+    """The strided forms past 4 GiB: the rounds kernel (an unaligned first packet) and the
+    tiny kernel (16-byte-aligned starts and stride)."""
+    n = 20_000
+    first = FOUR_G - 64 * 10_000 + first_adj
     want_arena = win.arena[first:first + n * stride].cpu().numpy()
     off = np.arange(n, dtype=np.uint64) * np.uint64(stride)
     want = oracle.batch(want_arena, off, np.full(n, L, dtype=np.uint32), None, complement=True)

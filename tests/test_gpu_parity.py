@@ -166,6 +166,51 @@ def test_strided_api(oracle):
         assert np.array_equal(host_u16(out), expect), (L, stride, first)
 
 
+def test_strided_tiny_packets(oracle):
+    """The strided tiny kernel (len <= 64 at 16-byte-aligned starts and stride): every length
+    1..64, strides from the packed one to 2048, packet counts that are not a multiple of 64,
+    with and without seeds and the complement, all-0xff bytes, packets past the arena's end
+    (rejected and counted), an unaligned arena pointer (the kernel's absolute alignment rule
+    then sends the batch to the rounds kernel) and overlapping packets (stride < len)."""
+    rng = O.splitmix64_words(0x7A1, 4096)
+    k = 0
+    for L in list(range(1, 65)) + [64, 48, 17]:
+        stride = 2048 if L % 5 == 0 else 16 if L % 3 == 0 else (L + 15) & ~15   # 16: overlapping packets
+        n = 64 * (1 + int(rng[k] % np.uint64(40))) + int(rng[k + 1] % np.uint64(64))
+        first = 16 * int(rng[k + 2] % np.uint64(8))
+        k += 3
+        arena_np = O.splitmix64_bytes(L * 7919, first + stride * n + 64)
+        if L in (48, 17):
+            arena_np[:] = 0xFF
+        arena = torch.from_numpy(arena_np.copy()).to(DEV)
+        sd_np = (O.splitmix64_words(L + 5, n) & np.uint64(0xFFFF)).astype(np.uint16)
+        off = first + np.arange(n, dtype=np.uint64) * np.uint64(stride)
+        for seeded, comp in ((True, True), (False, False)):
+            out = csum_batch_strided(arena, n, stride, L, first_off=first, seed=to_dev(sd_np, np.int16) if seeded else None,
+                                     complement=comp)
+            expect = oracle.batch(arena_np, off, np.full(n, L, dtype=np.uint32), sd_np if seeded else None,
+                                  complement=comp)
+            assert np.array_equal(host_u16(out), expect), (L, stride, first, seeded)
+    # past the arena's end: the last packets rejected, counted, 0
+    L, stride, n = 64, 64, 1000
+    arena_np = O.splitmix64_bytes(3, 64 * 990 + 20)
+    arena = torch.from_numpy(arena_np.copy()).to(DEV)
+    bad = torch.zeros(1, dtype=torch.int32, device=DEV)
+    got = host_u16(csum_batch_strided(arena, n, stride, L, complement=True, bad=bad))
+    off = np.arange(990, dtype=np.uint64) * np.uint64(64)
+    assert np.array_equal(got[:990], oracle.batch(arena_np, off, np.full(990, L, np.uint32), None, complement=True))
+    assert (got[990:] == 0).all() and int(bad.item()) == 10
+    # an unaligned arena pointer, and overlapping packets
+    base = torch.from_numpy(O.splitmix64_bytes(9, 70_000)).to(DEV)
+    for view_off, L, stride in ((8, 64, 64), (0, 64, 32), (0, 40, 16)):
+        view = base[view_off:]
+        n = 1000
+        got = host_u16(csum_batch_strided(view, n, stride, L, complement=True))
+        host = view.cpu().numpy()
+        off = np.arange(n, dtype=np.uint64) * np.uint64(stride)
+        assert np.array_equal(got, oracle.batch(host, off, np.full(n, L, np.uint32), None, complement=True))
+
+
 @pytest.mark.parametrize("name", ["c2_64B", "c3_1500B", "c4_9000B", "c5_imix"])
 def test_full_size_configs_bit_exact(oracle, name):
     """Every packet of every BASELINE.json GPU config, bit-exact against the C oracle."""

@@ -90,6 +90,8 @@ def main():
                          "fragment in its own 512-byte buffer (NetBuffer, buf.rs:50), ceil(L/512) per packet, "
                          "the buffers in order (a packet's fragments adjacent); netbuf_shuffled: the same "
                          "buffers in a random order (no two fragments adjacent)")
+    ap.add_argument("--tx-frags", default="0,512", help="chain_fill: payload fragment sizes (0 = one fragment)")
+    ap.add_argument("--tx-modes", default="plain,runs,txpacked", help="chain_fill: hint flags to time")
     args = ap.parse_args()
     ops = set(args.ops.split(","))
     dev = torch.device("cuda:0")
@@ -111,7 +113,7 @@ def main():
                     r[key + ("_runs" if runs else "")] = bench_chain(b, lay, dev, args, runs) if cl == "packed" else \
                         bench_chain_netbuf(lay, dev, args, shuffled=cl == "netbuf_shuffled", runs=runs)
         if "chain_fill" in ops:
-            for frag in (0, 512):
+            for frag in (int(x) for x in args.tx_frags.split(",")):
                 r.update(bench_chain_fill(cfg, dev, args, frag))
         if "fill" in ops:
             ms = timed(lambda: csum_fill(b.arena, b.off, b.length, b.seed, field_off=16), args.steps, args.rounds)
@@ -200,7 +202,8 @@ def bench_chain_fill(cfg, dev, args, frag):
     hint = int(round(pay / nf))
     tag = "tx" if frag == 0 else f"tx{frag}"
     res = {}
-    for runs, txp in ((False, False), (True, False), (False, True)):
+    modes = {"plain": (False, False), "runs": (True, False), "txpacked": (False, True)}
+    for runs, txp in (modes[m] for m in args.tx_modes.split(",")):
         sfx = "_runs" if runs else "_txpacked" if txp else ""
         ms = timed(lambda: csum_chain_fill(arena, d_fo, d_fl, d_first, seed, field_off=t.field, out=out,
                                            frag_len_hint=hint, runs=runs, tx_packed=txp), args.steps, args.rounds)
