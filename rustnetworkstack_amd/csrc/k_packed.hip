@@ -11,33 +11,26 @@ namespace rns {
 // kernels carry no packed-form code): the mixed kernel, or for tiny packets the
 // rounds kernel with pick_shape's G=4, U=1 shape.
 // Receive verify's stream launch: one wave per 64-datagram unit.
-#ifndef RNS_RX_ROWS  // A/B knob (round 5): 1 = receive verify through the rows kernel, 0 = the stream kernel
-#define RNS_RX_ROWS 1
-#endif
 #ifndef RNS_RX_ROWS_D  // rows in flight of the receive form
 #define RNS_RX_ROWS_D 8
 #endif
+// Packed receive verify: the rows receive kernel (round 5: IMIX 468.1 -> 449.2-450.3 us, c3
+// 230.4 -> 225.0-226.2 per step against the stream kernel), except for arenas of ACK-sized
+// datagrams (at most 128 arena bytes per datagram), where the stream kernel's ACK path measured
+// faster (14.54-14.64 vs 15.03-15.25 us per isolated dispatch; sessions r05c-r05h).
 int launch_stream_rx(const CsumArgs &a, hipStream_t st)
 {
     const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);
     constexpr bool NT = RNS_STREAM_NT != 0;
-    // ACK-sized datagrams (at most 128 arena bytes per datagram): the instantiation without the rows
-    const bool ack = a.arena_bytes / a.n <= 128;
-    if (RNS_RX_ROWS) {
-        const bool buf = buf_records(a) < kOobOffset;
-        if (ack && buf)
-            hipLaunchKernelGGL((csum_rows_rx_kernel<NT, true, RNS_RX_ROWS_D, true>), grid, block, 0, st, a);
-        else if (ack)
-            hipLaunchKernelGGL((csum_rows_rx_kernel<NT, false, RNS_RX_ROWS_D, true>), grid, block, 0, st, a);
-        else if (buf)
-            hipLaunchKernelGGL((csum_rows_rx_kernel<NT, true, RNS_RX_ROWS_D>), grid, block, 0, st, a);
-        else
-            hipLaunchKernelGGL((csum_rows_rx_kernel<NT, false, RNS_RX_ROWS_D>), grid, block, 0, st, a);
-    } else if (buf_records(a) < kOobOffset) {
+    const bool ack = a.arena_bytes / a.n <= 128, buf = buf_records(a) < kOobOffset;
+    if (ack && buf)
         hipLaunchKernelGGL((csum_stream_kernel<NT, true>), grid, block, 0, st, a);
-    } else {
+    else if (ack)
         hipLaunchKernelGGL((csum_stream_kernel<NT, false>), grid, block, 0, st, a);
-    }
+    else if (buf)
+        hipLaunchKernelGGL((csum_rows_rx_kernel<NT, true, RNS_RX_ROWS_D>), grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL((csum_rows_rx_kernel<NT, false, RNS_RX_ROWS_D>), grid, block, 0, st, a);
     return hip_status(hipGetLastError());
 }
 

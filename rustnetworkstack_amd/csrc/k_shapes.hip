@@ -115,12 +115,11 @@ template int dispatch<false>(const CsumArgs &, uint32_t, uint32_t, uint32_t, uin
 template int dispatch<true>(const CsumArgs &, uint32_t, uint32_t, uint32_t, uint32_t, hipStream_t);
 
 // Tiny fixed-size packets at a fixed 16-byte-aligned stride: csum_strided_tiny_kernel.
-#ifndef RNS_STRIDED_TINY_B  // 64-packet batches per wave
-#define RNS_STRIDED_TINY_B 1
-#endif
 int launch_strided_tiny(const CsumArgs &a, hipStream_t st)
 {
-    constexpr int B = RNS_STRIDED_TINY_B;
+    // two 64-packet batches per wave: c2 isolated 12.56-12.59 -> 12.24-12.29 us, per step equal
+    // (10.76-11.5 / 10.97-11.14); four: 13.55-13.65 (session r05h)
+    constexpr int B = 2;
     const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 64 * B - 1) / (64 * B))), block(64);
     if (buf_records(a) < kOobOffset)
         hipLaunchKernelGGL((csum_strided_tiny_kernel<true, B>), grid, block, 0, st, a);

@@ -202,11 +202,9 @@ int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uin
     a.fixed_len = len;
     a.n = n;
     a.flags = flags;
-#ifndef RNS_STRIDED_TINY  // A/B knob (round 5): 0 = tiny strided packets through the rounds kernel
-#define RNS_STRIDED_TINY 1
-#endif
-    // packets of at most 64 bytes at 16-byte-aligned starts: the strided tiny kernel (c2)
-    if (RNS_STRIDED_TINY && len != 0 && len <= 64 && ((first_off + a.base_adjust) & 15) == 0 && (stride & 15) == 0)
+    // packets of at most 64 bytes at 16-byte-aligned starts: the strided tiny kernel (c2 isolated
+    // 12.83-12.94 -> 12.24-12.29 us against the rounds kernel: sessions r05g, r05h)
+    if (len != 0 && len <= 64 && ((first_off + a.base_adjust) & 15) == 0 && (stride & 15) == 0)
         return launch_strided_tiny(a, static_cast<hipStream_t>(stream));
     const Shape sh = pick_shape(len);
     return dispatch<true>(a, sh.variant, sh.G, sh.U, sh.max_blocks, static_cast<hipStream_t>(stream));
@@ -767,11 +765,14 @@ const char *rns_csum_shape_name(uint32_t len_hint)
 const char *rns_build_info(void)
 {
     return "rns_checksum abi=1 offload-arch=gfx950 kernels=csum_rows_kernel (packed form: 1 KiB rows per 64-packet "
-           "region, owners capture two region prefixes and sum their own end chunk), csum_stream_kernel (receive "
-           "verify: LDS header stash; ACK-sized units owner-loaded), csum_mixed_kernel "
-           "(per-wave size-class sort; verify / fill / transmit-finalize stash modes), csum_rounds_kernel, "
-           "csum_batch_kernel, csum_chain_kernel (one pass, per-fragment fold) (v_sad_u16 LE sums, v_dot4 BE sums past "
-           "128 KiB, wave64, DPP reductions)";
+           "region, owners capture two region prefixes and sum their own end chunk; fill mode), csum_rows_rx_kernel "
+           "(packed receive verify: the rows plus each owner's header chunks loaded a group ahead), csum_stream_kernel "
+           "(receive verify of ACK-sized arenas: owners load their datagrams whole), csum_txrows_kernel (transmit-shaped "
+           "chains: packed payload rows + owner-loaded head fragments; head-fragment fill), csum_strided_tiny_kernel "
+           "(fixed-size packets <= 64 B at a fixed stride), csum_mixed_kernel (per-wave size-class sort; verify / fill / "
+           "transmit-finalize stash modes), csum_rounds_kernel, csum_batch_kernel, csum_chain_kernel (one pass, "
+           "per-fragment fold; head-fragment fill) (v_sad_u16 LE sums, v_dot4 BE sums past 128 KiB, wave64, DPP "
+           "reductions)";
 }
 
 int rns_device_count(void)

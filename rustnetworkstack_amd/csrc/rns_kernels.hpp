@@ -1953,22 +1953,17 @@ __device__ __forceinline__ uint4 keep_first(uint4 v, uint32_t c)
 #ifndef RNS_STREAM_NT  // nontemporal loads in the stream kernel
 #define RNS_STREAM_NT 1
 #endif
-#ifndef RNS_STREAM_D  // rows (1 KiB loads) in flight per wave (8 since the rows start line-aligned:
-#define RNS_STREAM_D 8   // IMIX verify 472.3-472.8 -> 468.0-470.3 us, c3 235.9 -> 234.5; 6: 476.9; r04af)
-#endif
-#ifndef RNS_STREAM_LINE_ALIGN  // receive verify's row stream from the 128-byte line below the region
-#define RNS_STREAM_LINE_ALIGN 1    // (IMIX verify 473.6-473.7 -> 469.5-471.5 us, c3 equal; session r04y)
-#endif
-#ifndef RNS_STREAM_RX_OCC  // waves/SIMD bound of the receive-verify instantiation (its finish needs registers)
-#define RNS_STREAM_RX_OCC 6
-#endif
 #ifndef RNS_STREAM_OUT_AUX  // cache-policy bits of the result buffer stores (17 = sc0 | sc1)
 #define RNS_STREAM_OUT_AUX 17
 #endif
 // Result stores: buffer stores with the policy bits above (arrays below 2^30 entries; larger
 // ones: nontemporal stores).  IMIX, isolated dispatch: plain stores 472 us, nontemporal
 // 454-461, sc0|sc1 455.9 (r03i, r03o; sc0 alone 474, sc1 457, sc1|nt 461-466, sc0|nt 459-460).
-constexpr int kStreamD = RNS_STREAM_D;
+// The stream kernel's rows in flight: 8 since its rows start line-aligned (IMIX verify 472.3-472.8
+// -> 468.0-470.3 us, c3 235.9 -> 234.5; 6: 476.9; r04af), and its waves/SIMD bound (its finish
+// needs registers).
+constexpr int kStreamD = 8;
+constexpr int kStreamRxOcc = 6;
 
 // Chunk i of the datagram of len bytes whose 16-byte-aligned chunk 0 is at byte offset off
 // (zero, with no load, for a chunk wholly past the end; the last chunk is not masked).
@@ -1998,7 +1993,7 @@ __device__ __forceinline__ uint4 own_chunk(const CsumArgs &a, __amdgpu_buffer_rs
 // kernel gave way to csum_rows_kernel in round 4; forms that gave a wave several units were
 // measured slower in round 3 and removed.)  One wave per 64-datagram unit.
 template <bool NT, bool BUF>
-__global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(const CsumArgs a)
+__global__ __launch_bounds__(64, kStreamRxOcc) void csum_stream_kernel(const CsumArgs a)
 {
     constexpr int kNS = 4;  // stash chunks per datagram (16-byte-aligned: its first 64 bytes)
     // entry bits: [31:17] row tag, [16] head chunk, [15:14] head index, [13] end chunk,
@@ -2065,9 +2060,9 @@ __global__ __launch_bounds__(64, RNS_STREAM_RX_OCC) void csum_stream_kernel(cons
     }
     if ((r0 & 15) == 0) {
         // ---- stream path ----
-        // (rows from the 128-byte line below the region, as csum_rows_kernel: RNS_ROWS_LINE_ALIGN)
+        // (rows from the 128-byte line below the region, as csum_rows_kernel)
         const uint32_t la = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a.arena) + r0) & 127u;
-        const uint32_t lead = (RNS_STREAM_LINE_ALIGN != 0 && la <= r0) ? la : 0u;
+        const uint32_t lead = la <= r0 ? la : 0u;  // (IMIX verify 473.6-473.7 -> 469.5-471.5 us: r04y)
         const uint64_t rb = r0 - lead;
         const uint32_t nrows = (total + lead + 1023) >> 10;
         tab[lane] = 0xFFFFFFFFu;  // tag 0x7FFF: never a row
@@ -2653,14 +2648,12 @@ __global__ __launch_bounds__(64) void csum_strided_tiny_kernel(const CsumArgs a)
 #ifndef RNS_ROWS_RX_OCC  // waves/SIMD bound of the receive form (its header chunks need registers)
 #define RNS_ROWS_RX_OCC 5
 #endif
-// ACK: the instantiation for arenas of ACK-sized datagrams (the host's guess from the arena
-// bytes per datagram): without the rows path it needs few registers and runs at 8 waves/SIMD;
-// a unit with a longer datagram still gets exact results from the per-datagram wave loop.
-#ifndef RNS_RX_ACK_OCC  // waves/SIMD bound of the ACK instantiation
-#define RNS_RX_ACK_OCC 8
-#endif
-template <bool NT, bool BUF, int D, bool ACK = false>
-__global__ __launch_bounds__(64, ACK ? RNS_RX_ACK_OCC : RNS_ROWS_RX_OCC) void csum_rows_rx_kernel(const CsumArgs a)
+// (Arenas of ACK-sized datagrams — at most 128 arena bytes per datagram — go to csum_stream_kernel,
+// whose identical ACK path measured faster there: 64-byte datagrams 14.54-14.64 us per isolated
+// dispatch against 15.03-15.25 for this kernel, at 6 or 8 waves/SIMD, with or without an LDS
+// reservation like the stream kernel's; sessions r05g, r05h.)
+template <bool NT, bool BUF, int D>
+__global__ __launch_bounds__(64, RNS_ROWS_RX_OCC) void csum_rows_rx_kernel(const CsumArgs a)
 {
     constexpr int kNS = 4;  // header chunks per datagram (16-byte-aligned: its first 64 bytes)
     const uint32_t lane = threadIdx.x;
@@ -2699,13 +2692,6 @@ __global__ __launch_bounds__(64, ACK ? RNS_RX_ACK_OCC : RNS_ROWS_RX_OCC) void cs
                 a.l4_out[p] = static_cast<uint16_t>(l4_res);
         }
     };
-#ifdef RNS_RX_ACK_LDS  // A/B experiment: reserve LDS per workgroup in the ACK instantiation
-    if constexpr (ACK) {
-        __shared__ uint4 pad_lds[RNS_RX_ACK_LDS / 16];
-        if (a.n == 0xFFFFFFFFu)
-            pad_lds[lane] = make_uint4(lane, 0, 0, 0);
-    }
-#endif
     if ((r0 & 15) == 0 && !__ballot(len > 64)) {
         // ---- ACK-sized unit: every owner takes its datagram whole ----
 #pragma unroll
@@ -2723,7 +2709,7 @@ __global__ __launch_bounds__(64, ACK ? RNS_RX_ACK_OCC : RNS_ROWS_RX_OCC) void cs
             mine = __builtin_amdgcn_sad_u16(x.w, 0, mine);
         }
         finish(0u, false);
-    } else if (!ACK && (r0 & 15) == 0) {
+    } else if ((r0 & 15) == 0) {
         // ---- the rows: T, and the owner's first 4 chunks loaded a group ahead ----
         const uint32_t c0 = excl >> 4;
         const uint32_t e = len ? (excl + len - 1) >> 4 : c0;
@@ -2734,8 +2720,7 @@ __global__ __launch_bounds__(64, ACK ? RNS_RX_ACK_OCC : RNS_ROWS_RX_OCC) void cs
                 own[i] = 16u * i < len ? keep_first(own[i], len - 16u * i) : make_uint4(0, 0, 0, 0);
         finish(0u, false);
     } else {
-        // ---- unaligned region (rare; ACK: a unit with a longer datagram): the whole wave sums
-        // one datagram at a time ----
+        // ---- unaligned region (rare): the whole wave sums one datagram at a time ----
         uint64_t todo = __ballot(len != 0 && ok);
         while (todo) {
             const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
