@@ -566,10 +566,19 @@ class GpuEngine:
         from rustnetworkstack_amd import _lib
         if self.op == "verify":
             if self.verify_packed:
-                return ("csum_stream_kernel<RX> (rns_rx_verify_packed_dev: 1 KiB rows + header stash; units of "
-                        "ACK-sized datagrams: owners load their datagrams whole)")
+                b = self.batches[0]
+                if (b.arena.numel() // max(self.layout.n, 1)) <= 128:
+                    return ("csum_stream_kernel (rns_rx_verify_packed_dev, an arena of ACK-sized datagrams: "
+                            "owners load their datagrams whole)")
+                return ("csum_rows_rx_kernel (rns_rx_verify_packed_dev: 1 KiB rows; owners load their headers "
+                        "a group of rows ahead)")
             return "csum_mixed_kernel<RX> (rns_rx_verify_dev: class-sorted data pass + header stash)"
         mean = self.layout.mean_len
+        if getattr(self, "strided", False):
+            st = self.batches[0].stride()
+            if st is not None and 0 < st[2] <= 64 and st[0] % 16 == 0 and st[1] % 16 == 0:
+                return ("csum_strided_tiny_kernel (rns_csum_batch_strided_dev, packets <= 64 B at 16-byte-aligned "
+                        "starts: 4 rows of 16 packets x 4 chunks per 64-packet batch, two batches per wave)")
         if self.packed and self.layout.n and int(self.layout.off[0]) % 16 == 0 and mean > 112:
             return ("csum_rows_kernel (packed form, 16-byte-aligned packets: one wave streams each 64-packet "
                     "block as 1 KiB rows; owners capture two region prefixes and sum their own end chunk)")
