@@ -2646,7 +2646,7 @@ __global__ __launch_bounds__(64) void csum_strided_tiny_kernel(const CsumArgs a)
 // per-datagram wave loop.
 // ---------------------------------------------------------------------------
 #ifndef RNS_ROWS_RX_OCC  // waves/SIMD bound of the receive form (its header chunks need registers)
-#define RNS_ROWS_RX_OCC 5
+#define RNS_ROWS_RX_OCC 6  // (78 VGPRs, no scratch; 5 with all 4 header chunks loaded with the rows)
 #endif
 // (Arenas of ACK-sized datagrams — at most 128 arena bytes per datagram — go to csum_stream_kernel,
 // whose identical ACK path measured faster there: 64-byte datagrams 14.54-14.64 us per isolated
@@ -2710,10 +2710,23 @@ __global__ __launch_bounds__(64, RNS_ROWS_RX_OCC) void csum_rows_rx_kernel(const
         }
         finish(0u, false);
     } else if ((r0 & 15) == 0) {
-        // ---- the rows: T, and the owner's first 4 chunks loaded a group ahead ----
+        // ---- the rows: T, and the owner's first chunks loaded a group ahead ----
         const uint32_t c0 = excl >> 4;
         const uint32_t e = len ? (excl + len - 1) >> 4 : c0;
-        mine = rows_region_sum<NT, BUF, D, kNS>(a, rsrc, recs, r0, total, c0, e, len, own);
+        // (3 header chunks with the rows, the 4th only where needed: 78 VGPRs, 6 waves/SIMD — IMIX
+        // 448.0-448.4 -> 444.8-445.0 us, c3 isolated 234.1-234.3 -> 232.6-232.7 against all 4 at 5
+        // waves/SIMD, session r05j)
+        mine = rows_region_sum<NT, BUF, D, 3>(a, rsrc, recs, r0, total, c0, e, len, own);
+        {
+            // bytes 48..63 belong to the header only of an IPv4 datagram with more than 28 bytes of
+            // options (IHL > 12); the IPv6 header is 40 bytes: those few owners load chunk 3 now
+            const uint32_t b0 = own[0].x & 0xffu;
+            const bool need = live && len > 48 && (b0 >> 4) == 4 && (b0 & 15u) > 12;
+            if (__ballot(need))
+                own[3] = need ? own_chunk<BUF>(a, rsrc, recs, start, len, 3) : make_uint4(0, 0, 0, 0);
+            else
+                own[3] = make_uint4(0, 0, 0, 0);
+        }
 #pragma unroll
         for (int i = 0; i < kNS; ++i)  // zeros past the datagram's end (the region's next bytes)
             if (16u * i + 16u > len)

@@ -20,7 +20,9 @@ def test_bench_verify_rejects_exactly_the_corrupted(config, steps):
     assert v["rejected_total"] == v["rejected_expected"]
     assert v["datagrams_total"] > 0
     assert line["metric"] == bench.METRIC_VERIFY
-    assert line["roofline"]["kernel"].startswith("csum_stream_kernel<RX>")
+    # packed receive arenas: the rows receive kernel, or for ACK-sized datagrams (c2) the stream kernel
+    want = "csum_stream_kernel" if config == "c2_64B" else "csum_rows_rx_kernel"
+    assert line["roofline"]["kernel"].startswith(want)
     assert 0 < line["roofline"]["frac"] < 1.0
     assert line["cpu_baseline"] is None
 
