@@ -5,10 +5,6 @@
 #define RNS_ROWS_DEEP_FROM 1024u
 #endif
 
-#ifndef RNS_RX_ACK_KERNEL  // ACK-sized arenas through csum_rx_ack_kernel (else the stream kernel's ACK path)
-#define RNS_RX_ACK_KERNEL 0
-#endif
-
 namespace rns {
 
 // The packed form's kernels (separate instantiations, so the explicit-descriptor
@@ -21,20 +17,14 @@ namespace rns {
 // Packed receive verify: the rows receive kernel (round 5: IMIX 468.1 -> 449.2-450.3 us, c3
 // 230.4 -> 225.0-226.2 per step against the stream kernel), except for arenas of ACK-sized
 // datagrams (at most 128 arena bytes per datagram), where the stream kernel's ACK path measured
-// faster (14.54-14.64 vs 15.03-15.25 us per isolated dispatch; sessions r05c-r05h).
+// faster (14.54-14.64 vs 15.03-15.25 us per isolated dispatch; sessions r05c-r05h; a kernel of
+// its own, 1 or 2 units per wave at 6-8 waves/SIMD: 15.2-19.5 against 14.7-14.9, r05n).
 int launch_stream_rx(const CsumArgs &a, hipStream_t st)
 {
     const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);
     constexpr bool NT = RNS_STREAM_NT != 0;
     const bool ack = a.arena_bytes / a.n <= 128, buf = buf_records(a) < kOobOffset;
-    if (ack && RNS_RX_ACK_KERNEL) {
-        constexpr int U = RNS_RX_ACK_U;
-        const dim3 g2(static_cast<uint32_t>(((static_cast<uint64_t>(a.n) + 63) / 64 + U - 1) / U));
-        if (buf)
-            hipLaunchKernelGGL((csum_rx_ack_kernel<true, U>), g2, block, 0, st, a);
-        else
-            hipLaunchKernelGGL((csum_rx_ack_kernel<false, U>), g2, block, 0, st, a);
-    } else if (ack && buf)
+    if (ack && buf)
         hipLaunchKernelGGL((csum_stream_kernel<NT, true>), grid, block, 0, st, a);
     else if (ack)
         hipLaunchKernelGGL((csum_stream_kernel<NT, false>), grid, block, 0, st, a);

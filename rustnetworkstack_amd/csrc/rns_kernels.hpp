@@ -2568,9 +2568,6 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : FILL ? RNS_ROWS_FILL_OCC : 8) voi
 // ds_bpermute per row and finishes (util.rs:88-106: the LE sum folded and byte-swapped — the
 // starts are even — plus the seed, folded).
 // ---------------------------------------------------------------------------
-#ifndef RNS_TINY_SEED_EARLY
-#define RNS_TINY_SEED_EARLY 1
-#endif
 template <bool BUF, int B>
 __global__ __launch_bounds__(64) void csum_strided_tiny_kernel(const CsumArgs a)
 {
@@ -2583,13 +2580,13 @@ __global__ __launch_bounds__(64) void csum_strided_tiny_kernel(const CsumArgs a)
     const uint32_t jb = 16u * j;
     const uint64_t start0 = a.first_off + a.base_adjust;
     // the seeds first, with the rows (issued where they are used they cost the wave a second
-    // memory latency after its rows: RNS_TINY_SEED_EARLY A/B)
+    // memory latency after its rows: 12.24-12.29 -> 12.06-12.08 us per isolated dispatch, r05m)
     uint32_t sd[B];
 #pragma unroll
     for (int b = 0; b < B; ++b) {
         const uint64_t p = (static_cast<uint64_t>(blockIdx.x) * B + b) * 64 + lane;
         sd[b] = 0;
-        if (RNS_TINY_SEED_EARLY && a.seed)
+        if (a.seed)
             sd[b] = a.seed[p < a.n ? p : a.n - 1];
     }
     uint4 v[B][4];
@@ -2633,8 +2630,7 @@ __global__ __launch_bounds__(64) void csum_strided_tiny_kernel(const CsumArgs a)
         if (p < a.n) {
             const uint64_t st = start0 + p * a.stride;
             const bool ok = st <= a.arena_bytes && L <= a.arena_bytes - st;
-            const uint32_t sdp = RNS_TINY_SEED_EARLY ? sd[b] : a.seed ? static_cast<uint32_t>(a.seed[p]) : 0u;
-            a.out[p] = finalize_bits(mine, false, false, sdp, ok, a.flags);  // 64 consecutive u16: one 128-byte store
+            a.out[p] = finalize_bits(mine, false, false, sd[b], ok, a.flags);  // 64 consecutive u16: one 128-byte store
         }
         if (a.bad) {
             const uint64_t st = start0 + p * a.stride;
@@ -2785,120 +2781,6 @@ __global__ __launch_bounds__(64, RNS_ROWS_RX_OCC) void csum_rows_rx_kernel(const
 }
 
 // ---------------------------------------------------------------------------
-// Receive verify of ACK-sized datagrams (packed arena, at most 64 bytes each): U 64-datagram
-// units per wave with every unit's descriptor loads, then every owner's 4 chunks, in flight
-// together (one memory latency per step for U units, not per unit).  A unit that is not
-// ACK-shaped (a longer datagram, an unaligned start) takes the exact wave loop.
-// ---------------------------------------------------------------------------
-#ifndef RNS_RX_ACK_U
-#define RNS_RX_ACK_U 2
-#endif
-#ifndef RNS_RX_ACK_OCC
-#define RNS_RX_ACK_OCC 8
-#endif
-template <bool BUF, int U>
-__global__ __launch_bounds__(64, RNS_RX_ACK_OCC) void csum_rx_ack_kernel(const CsumArgs a)
-{
-    constexpr int kNS = 4;
-    const uint32_t lane = threadIdx.x;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
-    const uint64_t recs = buf_records(a);
-    const uint64_t units = (static_cast<uint64_t>(a.n) + 63) / 64;
-    const uint32_t zero_v = __builtin_amdgcn_mbcnt_lo(0u, 0u);
-    uint64_t r0v[U];
-    uint32_t len[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint64_t unit = static_cast<uint64_t>(blockIdx.x) * U + u;
-        const uint64_t p = unit * 64 + lane;
-        r0v[u] = a.blk_off[(unit < units ? unit : units - 1) + zero_v];
-        len[u] = p < a.n ? static_cast<uint32_t>(a.len16[p]) : 0u;
-    }
-    uint64_t start[U];
-    bool ack[U];
-    uint4 own[U][kNS + 1];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint64_t r0 =
-            ((static_cast<uint64_t>(
-                  static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(r0v[u] >> 32))))
-              << 32) |
-             static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(r0v[u])))) +
-            a.base_adjust;
-        const uint32_t pad = (len[u] + a.align_mask) & ~a.align_mask;
-        const uint32_t excl = wave_incl_scan(pad) - pad;
-        start[u] = r0 + excl;
-        ack[u] = (r0 & 15) == 0 && !__ballot(len[u] > 64);
-#pragma unroll
-        for (int i = 0; i < kNS; ++i)  // (a unit that is not ACK-shaped loads nothing here)
-            own[u][i] = own_chunk<BUF>(a, rsrc, recs, start[u], ack[u] ? len[u] : 0u, i);
-        own[u][kNS] = make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint64_t p = (static_cast<uint64_t>(blockIdx.x) * U + u) * 64 + lane;
-        const bool live = p < a.n;
-        const uint32_t L = len[u];
-        const bool ok = start[u] <= a.arena_bytes && L <= a.arena_bytes - start[u];
-        uint32_t mine = 0, s0 = 0;
-        bool odd = false;
-        if (ack[u]) {
-#pragma unroll
-            for (int i = 0; i < kNS; ++i) {
-                uint4 x = own[u][i];
-                if (16u * i + 16u > L)  // rx_finish sees zeros past the end
-                    x = 16u * i < L ? keep_first(x, L - 16u * i) : make_uint4(0, 0, 0, 0);
-                own[u][i] = x;
-                mine = __builtin_amdgcn_sad_u16(x.x, 0, mine);
-                mine = __builtin_amdgcn_sad_u16(x.y, 0, mine);
-                mine = __builtin_amdgcn_sad_u16(x.z, 0, mine);
-                mine = __builtin_amdgcn_sad_u16(x.w, 0, mine);
-            }
-        } else {
-            // ---- not ACK-shaped: the whole wave sums one datagram at a time ----
-            const uint64_t st0 = start[u];
-            uint64_t todo = __ballot(L != 0 && ok);
-            while (todo) {
-                const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
-                todo &= todo - 1;
-                const uint64_t st =
-                    (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(st0 >> 32), o)))
-                     << 32) |
-                    static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(st0), o));
-                const Pkt k = make_pkt(st, __builtin_amdgcn_readlane(L, o));
-                uint32_t acc = 0;
-                for (uint32_t cc = 0; cc < k.nch; cc += 64) {
-                    uint4 w[1];
-                    issue_pass<64, 1, false, BUF, 1>(a, rsrc, k, cc + lane, w);
-                    mask_edges<64, 1, 1>(k, cc + lane, w);
-                    acc = sum_le<1, 1>(w, acc);
-                }
-                const uint32_t sum = group_allreduce<64>(acc);
-                mine = lane == o ? sum : mine;
-            }
-            const uint64_t b0 = st0 & ~15ull;
-            s0 = static_cast<uint32_t>(st0 & 15);
-            odd = st0 & 1;
-#pragma unroll
-            for (int i = 0; i < kNS + 1; ++i) {
-                const uint4 x = own_chunk<BUF>(a, rsrc, recs, b0, (L && ok) ? s0 + L : 0u, i);
-                const int lo = static_cast<int>(s0) - 16 * i, hi = static_cast<int>(s0 + L) - 16 * i;
-                own[u][i] = make_uint4(keep_bytes(x.x, lo, hi, 0), keep_bytes(x.y, lo, hi, 4), keep_bytes(x.z, lo, hi, 8),
-                                       keep_bytes(x.w, lo, hi, 12));
-            }
-        }
-        uint32_t l4_res = 0;
-        const uint8_t stv = rx_finish<kNS + 1>(a, own[u], mine, s0, L, odd, false, live && ok && L != 0, l4_res);
-        if (live) {
-            a.status[p] = stv;
-            if (a.l4_out)
-                a.l4_out[p] = static_cast<uint16_t>(l4_res);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Transmit-shaped chains (RNS_FLAG_CHAIN_TX_PACKED; rns_csum_chain_dev and
 // rns_csum_chain_fill_dev).  What tcp_output checksums (tcp.rs:938-973) is a head fragment
 // (the TCP header alloc_header prepended, buf.rs:262-291) followed by the payload.  A batching
@@ -2924,9 +2806,6 @@ __global__ __launch_bounds__(64, RNS_RX_ACK_OCC) void csum_rx_ack_kernel(const C
 // ---------------------------------------------------------------------------
 #ifndef RNS_TXROWS_OCC  // waves/SIMD bound of the transmit-rows kernel
 #define RNS_TXROWS_OCC 5  // (zero scratch at 86-89 VGPRs; 6 spills 32-116 B/lane)
-#endif
-#ifndef RNS_TX_HEAD_REWRITE
-#define RNS_TX_HEAD_REWRITE 0
 #endif
 constexpr uint32_t kTxHeadMax = 64;  // (head start & 15) + head length: at most 4 chunks
 
@@ -3117,56 +2996,7 @@ __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const C
     // (field stores as buffer stores with the result stores' sc0|sc1 bits: IMIX 604.4 -> 598.4 us,
     // c3 251.0 -> 245.7 against ordinary stores; nontemporal 595.8 / 246.4: session r05e)
     if constexpr (FILL) {
-        if (RNS_TX_HEAD_REWRITE && fast) {
-            // rewrite each head whole, its field patched: the wave's heads are one run of lines,
-            // so the L2 evicts whole lines (no partial-line writes behind the field stores)
-            if (okp) {
-                const uint64_t hb = o[0] & ~15ull;
-                const uint32_t hs = static_cast<uint32_t>(o[0] & 15u), span = hs + hl;
-                const uint32_t q0 = hs + fo, q1 = q0 + 1u;
-                uint8_t *w8 = const_cast<uint8_t *>(a.arena);
-                constexpr int kHeadAux = RNS_TX_HEAD_REWRITE == 2 ? RNS_STREAM_OUT_AUX : 0;
-#pragma unroll
-                for (uint32_t i = 0; i < 4; ++i) {
-                    if (16u * i >= span)
-                        continue;
-                    uint4 x = own_chunk<BUF>(a, rsrc, recs, hb, span, i);
-                    uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-                    for (uint32_t d = 0; d < 4; ++d) {
-                        const uint32_t b = 16u * i + 4u * d;
-                        if (q0 >= b && q0 < b + 4u)
-                            w[d] = (w[d] & ~(0xffu << ((q0 - b) * 8u))) | (((r >> 8) & 0xffu) << ((q0 - b) * 8u));
-                        if (q1 >= b && q1 < b + 4u)
-                            w[d] = (w[d] & ~(0xffu << ((q1 - b) * 8u))) | ((r & 0xffu) << ((q1 - b) * 8u));
-                    }
-                    const uint64_t cb = hb + 16u * i;
-                    if (hs <= 16u * i && span >= 16u * i + 16u) {
-                        if constexpr (BUF)
-                            __builtin_amdgcn_raw_buffer_store_b128(u32x4{w[0], w[1], w[2], w[3]}, rsrc,
-                                                                   static_cast<uint32_t>(cb), 0, kHeadAux);
-                        else
-                            *reinterpret_cast<uint4 *>(w8 + cb) = make_uint4(w[0], w[1], w[2], w[3]);
-                        continue;
-                    }
-#pragma unroll
-                    for (uint32_t d = 0; d < 4; ++d) {
-                        const uint32_t b = 16u * i + 4u * d;
-                        if (hs <= b && span >= b + 4u) {
-                            if constexpr (BUF)
-                                __builtin_amdgcn_raw_buffer_store_b32(w[d], rsrc, static_cast<uint32_t>(cb + 4u * d), 0, kHeadAux);
-                            else
-                                *reinterpret_cast<uint32_t *>(w8 + cb + 4u * d) = w[d];
-                        } else {
-#pragma unroll
-                            for (uint32_t k = 0; k < 4; ++k)
-                                if (b + k >= hs && b + k < span)
-                                    w8[cb + 4u * d + k] = static_cast<uint8_t>(w[d] >> (8u * k));
-                        }
-                    }
-                }
-            }
-        } else if (okp) {  // set_be16(&mut header[fo..fo + 2], result): the head fragment's bytes
+        if (okp) {  // set_be16(&mut header[fo..fo + 2], result): the head fragment's bytes
             uint8_t *w8 = const_cast<uint8_t *>(a.arena);
             const uint64_t fp = o[0] + fo;
             if (fp & 1) {
