@@ -1702,6 +1702,9 @@ constexpr int chain_occ()
 // freed per workgroup, as for the mixed kernel's stash modes: IMIX chains 640 -> 608 us
 // packed, 839 -> 771 us in 512-byte buffers, c3 equal (profiles/r02_block_ab.json).
 constexpr int kChainBlock = 64;
+#ifndef RNS_CHAIN_WINDOW  // arenas of 4 GiB or more: buffer loads through a per-pass window
+#define RNS_CHAIN_WINDOW 1
+#endif
 // RUNS: the RNS_FLAG_CHAIN_RUNS instantiation (buffer path only).  A separate kernel:
 // compiled into the plain one, the run check cost it ~5 % (registers) even unused.
 template <bool NT, bool BUF, uint32_t KMAX, bool RUNS = false, bool FILL = false, int OCC = 0>
@@ -1806,8 +1809,35 @@ __global__ __launch_bounds__(kChainBlock, (chain_occ<NT, BUF, KMAX, RUNS, FILL, 
             }
             const bool big = d_len > kNoWrapBytes, odd = d_start & 1;
             uint32_t pos;
-            const uint32_t w =
-                wave_class_pass<NT, BUF, kStashNone, kChainTiny && !NT>(a, rsrc, d_start, d_len, 0u, lane, nullptr, pos);
+            uint32_t w;
+            if constexpr (!BUF && RNS_CHAIN_WINDOW) {
+                // arenas of 4 GiB or more: a pass whose 64 fragments lie within one window below
+                // the buffer range (NetBuffers in order: 64 consecutive 512-byte buffers) loads
+                // through a buffer descriptor based at the window's 16-byte-aligned start (IMIX
+                // in 512-byte NetBuffers, a 6.4 GB arena: 751-753 -> 700-701 us; shuffled buffers,
+                // every pass 64-bit: 780-782 -> 793-795, the two paths' code; sessions r05p, r05q)
+                const uint32_t lo_hi = d_len ? static_cast<uint32_t>(d_start >> 32) : 0xFFFFFFFFu;
+                const uint32_t wlh = wave_min_u32(lo_hi);
+                const uint32_t wll = wave_min_u32(d_len && lo_hi == wlh ? static_cast<uint32_t>(d_start) & ~15u : 0xFFFFFFFFu);
+                const uint64_t end = d_len ? d_start + d_len : 0;
+                const uint32_t ehi = wave_max_u32(static_cast<uint32_t>(end >> 32));
+                const uint32_t elo = wave_max_u32(static_cast<uint32_t>(end >> 32) == ehi ? static_cast<uint32_t>(end) : 0u);
+                const uint64_t wlo = (static_cast<uint64_t>(wlh) << 32) | wll, whi = (static_cast<uint64_t>(ehi) << 32) | elo;
+                if (whi <= wlo || whi - wlo <= kOobOffset - 4096u) {  // (no fragment: whi = 0)
+                    const uint64_t wb = whi > wlo ? wlo : 0;
+                    const uint64_t recs_w = buf_records(a) - wb;
+                    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+                        const_cast<uint8_t *>(a.arena) + wb, static_cast<short>(0),
+                        static_cast<int>(recs_w < kOobOffset ? recs_w : kOobOffset), 0x00020000);
+                    w = wave_class_pass<NT, true, kStashNone, kChainTiny && !NT>(a, rw, d_len ? d_start - wb : 0, d_len, 0u,
+                                                                                  lane, nullptr, pos);
+                } else {
+                    w = wave_class_pass<NT, false, kStashNone, kChainTiny && !NT>(a, rsrc, d_start, d_len, 0u, lane, nullptr,
+                                                                                   pos);
+                }
+            } else {
+                w = wave_class_pass<NT, BUF, kStashNone, kChainTiny && !NT>(a, rsrc, d_start, d_len, 0u, lane, nullptr, pos);
+            }
             uint32_t g = w;  // big: BE sum mod 2^32; else the folded BE sum (RFC 1071 §2(B), as finalize_bits)
             if (!big) {
                 const uint32_t x = fold16(w);

@@ -10,8 +10,9 @@ translated), and for the in-place fills every byte of every window is compared.
 Entries covered: the packed checksum (rows kernel D = 8 and D = 16, the tiny rounds
 kernel, the unaligned-packing class kernel, a first block at an odd offset), the strided
 form, the packed and explicit transmit fills, packed and explicit receive verify, the
-transmit finalize, fragment chains (nontemporal and temporal class passes; the runs hint,
-which is ignored past 4 GiB) and the head-fragment chain fill.  Reference: util.rs:88-119,
+transmit finalize, fragment chains (nontemporal and temporal class passes, each through a
+buffer window based at its pass's fragments and through 64-bit loads for passes spanning more
+than 4 GiB; the runs hint, which is ignored past 4 GiB) and the head-fragment chain fill.  Reference: util.rs:88-119,
 tcp.rs:838-850 / 957-973, udp.rs:158-171, icmp.rs:46-112, ip.rs:76-80 / 158-159.
 """
 import numpy as np
@@ -366,6 +367,37 @@ def test_chains(oracle, win, hint, runs):
                               dev(seeds, np.int16), complement=True, frag_len_hint=hint, runs=runs))
     diff = np.flatnonzero(got != want)
     assert diff.size == 0, [(int(i), int(got[i]), int(want[i])) for i in diff[:5]]
+
+
+def interleave_packets(off, mini_off, ln, first, order):
+    """The same chains with the packets in a new order (fragment arrays rebuilt to match)."""
+    nf = np.diff(first.astype(np.int64))
+    idx = np.concatenate([np.arange(first[p], first[p + 1]) for p in order])
+    new_first = np.concatenate([[0], np.cumsum(nf[order])]).astype(np.uint32)
+    return off[idx], mini_off[idx], ln[idx], new_first
+
+
+@pytest.mark.parametrize("hint", [512, 100])
+def test_chains_far_apart(oracle, win, hint):
+    """Consecutive packets alternate between the first and the last window: every 64-fragment
+    pass spans more than 4 GiB, so none fits one buffer window (the 64-bit loads); then the
+    same packets window by window (every pass in one window: buffer loads from its base)."""
+    off, mini_off, ln, first = chain_windows(win, 1500, 3 + hint, 2 * hint)
+    n = first.size - 1
+    a = np.arange(0, 1500)
+    c = np.arange(3000, 4500)
+    order = np.empty(3000, dtype=np.int64)
+    order[0::2] = a
+    order[1::2] = c
+    for o in (order, np.arange(n)):
+        o_off, o_mini, o_ln, o_first = interleave_packets(off, mini_off, ln, first, o)
+        m = o_first.size - 1
+        seeds = (O.splitmix64_words(0xCD + hint, m) & np.uint64(0xFFFF)).astype(np.uint16)
+        want = oracle.chain_batch(np.concatenate(win.orig), o_mini, o_ln, o_first, seeds, complement=True)
+        got = host_u16(csum_chain(win.arena, dev(o_off, np.int64), dev(o_ln, np.int32), dev(o_first, np.int32),
+                                  dev(seeds, np.int16), complement=True, frag_len_hint=hint))
+        diff = np.flatnonzero(got != want)
+        assert diff.size == 0, [(int(i), int(got[i]), int(want[i])) for i in diff[:5]]
 
 
 @pytest.mark.parametrize("txp", [False, True])
