@@ -2243,6 +2243,9 @@ __global__ __launch_bounds__(64, kStreamRxOcc) void csum_stream_kernel(const Csu
 // a.arena) and holds total bytes (a multiple of 16; ceil(total / 1 KiB) rows): the lane's packet covers chunks c0..e of the region (its
 // start 16-byte aligned, len bytes, len 0: none).  Returns the packet's LE word sum (pairs by
 // absolute parity).  csum_rows_kernel's aligned path and the chain kernel's runs (below).
+#ifndef RNS_ROWS_WINDOW  // arenas of 4 GiB or more: the rows through a buffer window (1) or 64-bit loads (0)
+#define RNS_ROWS_WINDOW 1
+#endif
 struct NoHook {
     __device__ __forceinline__ void operator()() const {}
 };
@@ -2390,6 +2393,32 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
     return len ? pb - pa + part : 0u;
 }
 
+// The region sum on any arena: past 4 GiB (BUF = false) through a buffer descriptor based at the
+// region's 128-byte line (a region is at most 64 packets of 64 KiB: far below the buffer range),
+// so the rows keep buffer loads with their range checks and cache-policy bits instead of 64-bit
+// addresses (per isolated dispatch, session r05s: 3M x 1500 B 815 -> 684 us, 16M IMIX 945 -> 864,
+// the transmit-packed chain checksum of 16M IMIX 1263 -> 945).
+template <bool NT, bool BUF, int D, int NH = 0, typename Hook = NoHook>
+__device__ __forceinline__ uint32_t rows_region_sum_any(const CsumArgs &a, const __amdgpu_buffer_rsrc_t rsrc, uint64_t recs,
+                                                       uint64_t r0, uint32_t total, uint32_t c0, uint32_t e, uint32_t len,
+                                                       uint4 *hv = nullptr, Hook after_first = Hook{})
+{
+    if constexpr (BUF || !RNS_ROWS_WINDOW) {
+        return rows_region_sum<NT, BUF, D, NH>(a, rsrc, recs, r0, total, c0, e, len, hv, after_first);
+    } else {
+        const uint32_t la = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a.arena) + r0) & 127u;
+        const uint64_t wb = la <= r0 ? r0 - la : 0;  // the line the rows start at (absolute alignment kept)
+        CsumArgs aw = a;
+        aw.arena = a.arena + wb;
+        aw.arena_bytes = a.arena_bytes - wb;
+        const uint64_t rw_recs = recs - wb;
+        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t *>(aw.arena), static_cast<short>(0),
+            static_cast<int>(rw_recs < kOobOffset ? rw_recs : static_cast<uint64_t>(kOobOffset)), 0x00020000);
+        return rows_region_sum<NT, true, D, NH>(aw, rw, rw_recs, r0 - wb, total, c0, e, len, hv, after_first);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Row stream with owner captures (round 4; the packed form's plain checksum for
 // 16-byte-aligned packets above the tiny class: c3, c4, IMIX).
@@ -2493,7 +2522,7 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : FILL ? RNS_ROWS_FILL_OCC : 8) voi
     if ((r0 & 15) == 0) {
         const uint32_t c0 = excl >> 4;
         const uint32_t e = len ? (excl + len - 1) >> 4 : c0;
-        mine = rows_region_sum<NT, BUF, D>(a, rsrc, recs, r0, total, c0, e, len);
+        mine = rows_region_sum_any<NT, BUF, D>(a, rsrc, recs, r0, total, c0, e, len);
     } else {
         // ---- unaligned region (rare): the whole wave sums one packet at a time ----
         const uint64_t start = r0 + excl;
@@ -2755,7 +2784,7 @@ __global__ __launch_bounds__(64, RNS_ROWS_RX_OCC) void csum_rows_rx_kernel(const
         // (3 header chunks with the rows, the 4th only where needed: 78 VGPRs, 6 waves/SIMD — IMIX
         // 448.0-448.4 -> 444.8-445.0 us, c3 isolated 234.1-234.3 -> 232.6-232.7 against all 4 at 5
         // waves/SIMD, session r05j)
-        mine = rows_region_sum<NT, BUF, D, 3>(a, rsrc, recs, r0, total, c0, e, len, own);
+        mine = rows_region_sum_any<NT, BUF, D, 3>(a, rsrc, recs, r0, total, c0, e, len, own);
         {
             // bytes 48..63 belong to the header only of an IPv4 datagram with more than 28 bytes of
             // options (IHL > 12); the IPv6 header is 40 bytes: those few owners load chunk 3 now
@@ -2960,7 +2989,7 @@ __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const C
         };
         uint32_t mine = 0;
         if (pm) {
-            mine = rows_region_sum<NT, BUF, D>(a, rsrc, recs, r0, total, c0, e, has_pay ? plen : 0u, nullptr, head);
+            mine = rows_region_sum_any<NT, BUF, D>(a, rsrc, recs, r0, total, c0, e, has_pay ? plen : 0u, nullptr, head);
         } else {
             head();
         }

@@ -37,6 +37,9 @@ DIAG_CONFIGS = {
     "d40B": dict(n=1 << 22, kind="fixed", length=40),
     "d576B": dict(n=1 << 21, kind="fixed", length=576),
     "d1000B": dict(n=1 << 20, kind="fixed", length=1000),
+    # past 4 GiB (the kernels' 64-bit-address forms): 3 x c3 and 2 x IMIX in one batch
+    "d1500B_big": dict(n=3 << 20, kind="fixed", length=1500),
+    "dimix_big": dict(n=1 << 24, kind="imix"),
 }
 IMIX_SIZES = (40, 576, 1500)  # 7:4:1
 
