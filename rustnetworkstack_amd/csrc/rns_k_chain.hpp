@@ -128,9 +128,6 @@ constexpr int chain_occ()
 // freed per workgroup, as for the mixed kernel's stash modes: IMIX chains 640 -> 608 us
 // packed, 839 -> 771 us in 512-byte buffers, c3 equal (profiles/r02_block_ab.json).
 constexpr int kChainBlock = 64;
-#ifndef RNS_CHAIN_WINDOW  // arenas of 4 GiB or more: buffer loads through a per-pass window
-#define RNS_CHAIN_WINDOW 1
-#endif
 // RUNS: the RNS_FLAG_CHAIN_RUNS instantiation (buffer path only).  A separate kernel:
 // compiled into the plain one, the run check cost it ~5 % (registers) even unused.
 template <bool NT, bool BUF, uint32_t KMAX, bool RUNS = false, bool FILL = false, int OCC = 0>
@@ -236,7 +233,7 @@ __global__ __launch_bounds__(kChainBlock, (chain_occ<NT, BUF, KMAX, RUNS, FILL, 
             const bool big = d_len > kNoWrapBytes, odd = d_start & 1;
             uint32_t pos;
             uint32_t w;
-            if constexpr (!BUF && RNS_CHAIN_WINDOW) {
+            if constexpr (!BUF) {
                 // arenas of 4 GiB or more: a pass whose 64 fragments lie within one window below
                 // the buffer range (NetBuffers in order: 64 consecutive 512-byte buffers) loads
                 // through a buffer descriptor based at the window's 16-byte-aligned start (IMIX

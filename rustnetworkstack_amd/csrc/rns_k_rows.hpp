@@ -110,7 +110,7 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : FILL ? RNS_ROWS_FILL_OCC : 8) voi
     if ((r0 & 15) == 0) {
         const uint32_t c0 = excl >> 4;
         const uint32_t e = len ? (excl + len - 1) >> 4 : c0;
-        mine = rows_region_sum_any<NT, BUF, D>(a, rsrc, recs, r0, total, c0, e, len);
+        mine = rows_region_sum<NT, BUF, D>(a, rsrc, recs, r0, total, c0, e, len);
     } else {
         // ---- unaligned region (rare): the whole wave sums one packet at a time ----
         const uint64_t start = r0 + excl;
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(64, RNS_ROWS_RX_OCC) void csum_rows_rx_kernel(const
         // (3 header chunks with the rows, the 4th only where needed: 78 VGPRs, 6 waves/SIMD — IMIX
         // 448.0-448.4 -> 444.8-445.0 us, c3 isolated 234.1-234.3 -> 232.6-232.7 against all 4 at 5
         // waves/SIMD, session r05j)
-        mine = rows_region_sum_any<NT, BUF, D, 3>(a, rsrc, recs, r0, total, c0, e, len, own);
+        mine = rows_region_sum<NT, BUF, D, 3>(a, rsrc, recs, r0, total, c0, e, len, own);
         {
             // bytes 48..63 belong to the header only of an IPv4 datagram with more than 28 bytes of
             // options (IHL > 12); the IPv6 header is 40 bytes: those few owners load chunk 3 now
@@ -577,7 +577,7 @@ __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const C
         };
         uint32_t mine = 0;
         if (pm) {
-            mine = rows_region_sum_any<NT, BUF, D>(a, rsrc, recs, r0, total, c0, e, has_pay ? plen : 0u, nullptr, head);
+            mine = rows_region_sum<NT, BUF, D>(a, rsrc, recs, r0, total, c0, e, has_pay ? plen : 0u, nullptr, head);
         } else {
             head();
         }

@@ -321,10 +321,7 @@ __global__ __launch_bounds__(64, kStreamRxOcc) void csum_stream_kernel(const Csu
 // The rows decomposition over one region that starts 16-byte aligned at r0 (an offset from
 // a.arena) and holds total bytes (a multiple of 16; ceil(total / 1 KiB) rows): the lane's packet covers chunks c0..e of the region (its
 // start 16-byte aligned, len bytes, len 0: none).  Returns the packet's LE word sum (pairs by
-// absolute parity).  csum_rows_kernel's aligned path and the chain kernel's runs (below).
-#ifndef RNS_ROWS_WINDOW  // arenas of 4 GiB or more: the rows through a buffer window (1) or 64-bit loads (0)
-#define RNS_ROWS_WINDOW 1
-#endif
+// absolute parity).  Used by csum_rows_kernel, csum_rows_rx_kernel and csum_txrows_kernel (rns_k_rows.hpp).
 struct NoHook {
     __device__ __forceinline__ void operator()() const {}
 };
@@ -333,10 +330,12 @@ struct NoHook {
 // NH > 0 (receive verify): the owner also loads its packet's first NH chunks into hv[] (those
 // inside the packet; the others read as zero), like its end chunk: a group of rows ahead of
 // the row that streams them, so each line is fetched once.
-template <bool NT, bool BUF, int D, int NH = 0, typename Hook = NoHook>
-__device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __amdgpu_buffer_rsrc_t rsrc, uint64_t recs,
-                                                   uint64_t r0, uint32_t total, uint32_t c0, uint32_t e, uint32_t len,
-                                                   uint4 *hv = nullptr, Hook after_first = Hook{})
+// Buffer loads only: rsrc covers the region (rows_region_sum below gives arenas of 4 GiB or
+// more a descriptor based at the region).
+template <bool NT, int D, int NH, typename Hook>
+__device__ __forceinline__ uint32_t rows_stream(const CsumArgs &a, const __amdgpu_buffer_rsrc_t rsrc, uint64_t recs,
+                                               uint64_t r0, uint32_t total, uint32_t c0, uint32_t e, uint32_t len,
+                                               uint4 *hv, Hook after_first)
 {
     {
         // start the row stream at the 128-byte line below the region (the few bytes before it
@@ -354,7 +353,6 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
     // the owner's end chunk (pulling it from its row instead, four ds_bpermute per row, measured
     // 2x slower: session r04g)
     uint4 endv = make_uint4(0, 0, 0, 0);
-    constexpr bool kLate = BUF;
     const uint32_t row_e = len ? e >> 6 : 0xFFFFFFFFu;
     // the owners load their end chunks a group of D rows ahead of the rows
     // that hold them (one exec-masked load per group: its line is then still in L2 when the row
@@ -364,57 +362,33 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
     for (int i = 0; i < NH; ++i)
         hv[i] = make_uint4(0, 0, 0, 0);
     auto load_end_late = [&](uint32_t k) {  // end chunks in rows [k, k + D)
-        if constexpr (kLate) {
-            if (row_e - k < static_cast<uint32_t>(D)) {
-                const uint32_t off = static_cast<uint32_t>(r0) + (e << 4);
-                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16u <= recs ? off : kOobOffset, 0, 0);
-                endv = make_uint4(x.x, x.y, x.z, x.w);
-            }
-            if constexpr (NH > 0) {  // the packet's first chunks, a group ahead of their row
-                if (row_h - k < static_cast<uint32_t>(D)) {
+        if (row_e - k < static_cast<uint32_t>(D)) {
+            const uint32_t off = static_cast<uint32_t>(r0) + (e << 4);
+            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16u <= recs ? off : kOobOffset, 0, 0);
+            endv = make_uint4(x.x, x.y, x.z, x.w);
+        }
+        if constexpr (NH > 0) {  // the packet's first chunks, a group ahead of their row
+            if (row_h - k < static_cast<uint32_t>(D)) {
 #pragma unroll
-                    for (int i = 0; i < NH; ++i) {
-                        const uint32_t off = static_cast<uint32_t>(r0) + ((c0 + i) << 4);
-                        const bool in = 16u * i < len && off + 16u <= recs;
-                        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, in ? off : kOobOffset, 0, 0);
-                        hv[i] = make_uint4(x.x, x.y, x.z, x.w);
-                    }
+                for (int i = 0; i < NH; ++i) {
+                    const uint32_t off = static_cast<uint32_t>(r0) + ((c0 + i) << 4);
+                    const bool in = 16u * i < len && off + 16u <= recs;
+                    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, in ? off : kOobOffset, 0, 0);
+                    hv[i] = make_uint4(x.x, x.y, x.z, x.w);
                 }
             }
         }
     };
-    if constexpr (!kLate) {
-#pragma unroll
-        for (int i = 0; i < NH; ++i)
-            hv[i] = own_chunk<BUF>(a, rsrc, recs, r0 + (static_cast<uint64_t>(c0) << 4), len, i);
-        const uint64_t off = r0 + (static_cast<uint64_t>(e) << 4);
-        const bool in = len != 0 && off + 16 <= recs;
-        if constexpr (BUF) {
-            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, in ? static_cast<uint32_t>(off) : kOobOffset,
-                                                                  0, 0);
-            endv = make_uint4(x.x, x.y, x.z, x.w);
-        } else {
-            const uint4 x = load_chunk<false>(a.arena + (in ? off : 0));
-            endv = in ? x : make_uint4(0, 0, 0, 0);
-        }
-    }
     __builtin_amdgcn_sched_barrier(0);
     const uint32_t vlane = lane << 4;
     uint4 v[D];
     auto issue = [&](uint32_t k, uint4 &dst) {  // row k: chunk 64k + lane of the region
-        if constexpr (BUF) {
-            // lanes past the region's end load nothing (a row past it: no traffic at all); the next
-            // unit's wave streams those bytes, often on another XCD's L2
-            const uint32_t rel = (k << 10) + vlane;
-            const uint32_t o = rel < total ? static_cast<uint32_t>(r0) + rel : kOobOffset;
-            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, NT ? kNtAux : 0);
-            dst = make_uint4(x.x, x.y, x.z, x.w);
-        } else {
-            const uint64_t off = r0 + (static_cast<uint64_t>(k) << 10) + vlane;
-            const bool in = k < nrows && off + 16 <= recs;
-            const uint4 x = load_chunk<NT>(a.arena + (in ? off : 0));
-            dst = in ? x : make_uint4(0, 0, 0, 0);
-        }
+        // lanes past the region's end load nothing (a row past it: no traffic at all); the next
+        // unit's wave streams those bytes, often on another XCD's L2
+        const uint32_t rel = (k << 10) + vlane;
+        const uint32_t o = rel < total ? static_cast<uint32_t>(r0) + rel : kOobOffset;
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, NT ? kNtAux : 0);
+        dst = make_uint4(x.x, x.y, x.z, x.w);
     };
     load_end_late(0);
 #pragma unroll
@@ -436,7 +410,7 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
         }
         return part;
     };
-    uint32_t part = kLate ? 0u : end_part();
+    uint32_t part = 0;
     // capture points: P(c0 - 1) and P(e - 1) (row, source lane); e == c0 takes the
     // start's point twice (the difference is 0), c0 == 0 never captures (P(-1) = 0)
     const uint32_t ca = c0 - 1u;
@@ -467,23 +441,23 @@ __device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __a
             carry += __builtin_amdgcn_readlane(inc, 63);
         }
     }
-    if constexpr (kLate)
-        part = end_part();
+    part = end_part();
     return len ? pb - pa + part : 0u;
 }
 
-// The region sum on any arena: past 4 GiB (BUF = false) through a buffer descriptor based at the
+// The region sum: on an arena below 4 GiB (BUF) through the arena's buffer descriptor; past 4 GiB
+// through a buffer descriptor based at the
 // region's 128-byte line (a region is at most 64 packets of 64 KiB: far below the buffer range),
 // so the rows keep buffer loads with their range checks and cache-policy bits instead of 64-bit
 // addresses (per isolated dispatch, session r05s: 3M x 1500 B 815 -> 684 us, 16M IMIX 945 -> 864,
 // the transmit-packed chain checksum of 16M IMIX 1263 -> 945).
 template <bool NT, bool BUF, int D, int NH = 0, typename Hook = NoHook>
-__device__ __forceinline__ uint32_t rows_region_sum_any(const CsumArgs &a, const __amdgpu_buffer_rsrc_t rsrc, uint64_t recs,
-                                                       uint64_t r0, uint32_t total, uint32_t c0, uint32_t e, uint32_t len,
-                                                       uint4 *hv = nullptr, Hook after_first = Hook{})
+__device__ __forceinline__ uint32_t rows_region_sum(const CsumArgs &a, const __amdgpu_buffer_rsrc_t rsrc, uint64_t recs,
+                                                   uint64_t r0, uint32_t total, uint32_t c0, uint32_t e, uint32_t len,
+                                                   uint4 *hv = nullptr, Hook after_first = Hook{})
 {
-    if constexpr (BUF || !RNS_ROWS_WINDOW) {
-        return rows_region_sum<NT, BUF, D, NH>(a, rsrc, recs, r0, total, c0, e, len, hv, after_first);
+    if constexpr (BUF) {
+        return rows_stream<NT, D, NH>(a, rsrc, recs, r0, total, c0, e, len, hv, after_first);
     } else {
         const uint32_t la = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a.arena) + r0) & 127u;
         const uint64_t wb = la <= r0 ? r0 - la : 0;  // the line the rows start at (absolute alignment kept)
@@ -494,7 +468,7 @@ __device__ __forceinline__ uint32_t rows_region_sum_any(const CsumArgs &a, const
         const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint8_t *>(aw.arena), static_cast<short>(0),
             static_cast<int>(rw_recs < kOobOffset ? rw_recs : static_cast<uint64_t>(kOobOffset)), 0x00020000);
-        return rows_region_sum<NT, true, D, NH>(aw, rw, rw_recs, r0 - wb, total, c0, e, len, hv, after_first);
+        return rows_stream<NT, D, NH>(aw, rw, rw_recs, r0 - wb, total, c0, e, len, hv, after_first);
     }
 }
 
