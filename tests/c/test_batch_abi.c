@@ -335,13 +335,16 @@ static int test_chain_fill(hipStream_t st)
     HIP_OK(hipMemcpy(d_flen, flen, nf * sizeof *flen, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(d_first, first, (npk + 1) * sizeof *first, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(d_seed, seed, npk * sizeof *seed, hipMemcpyHostToDevice));
-    const uint32_t hints[2] = {512u, 100u};
-    for (int h = 0; h < 2; ++h) {
+    /* the chain kernel at two hints, then the transmit-rows kernel (RNS_FLAG_CHAIN_TX_PACKED:
+     * these scattered payloads take its exact per-packet loop) */
+    const uint32_t hints[3] = {512u, 100u, 512u};
+    const uint32_t flags[3] = {RNS_FLAG_COMPLEMENT, RNS_FLAG_COMPLEMENT, RNS_FLAG_COMPLEMENT | RNS_FLAG_CHAIN_TX_PACKED};
+    for (int h = 0; h < 3; ++h) {
         HIP_OK(hipMemcpy(d_arena, arena, bytes, hipMemcpyHostToDevice));
         HIP_OK(hipMemset(d_bad, 0, sizeof *d_bad));
         CHECK(rns_csum_chain_fill_dev(d_arena, bytes, d_foff, d_flen, nf, d_first, d_seed, NULL, fo, d_out, npk,
-                                      RNS_FLAG_COMPLEMENT, hints[h], d_bad, st) == RNS_OK,
-              "rns_csum_chain_fill_dev hint %u", hints[h]);
+                                      flags[h], hints[h], d_bad, st) == RNS_OK,
+              "rns_csum_chain_fill_dev hint %u flags %x", hints[h], flags[h]);
         HIP_OK(hipStreamSynchronize(st));
         HIP_OK(hipMemcpy(got, d_out, npk * sizeof *got, hipMemcpyDeviceToHost));
         HIP_OK(hipMemcpy(after, d_arena, bytes, hipMemcpyDeviceToHost));
@@ -354,6 +357,81 @@ static int test_chain_fill(hipStream_t st)
         CHECK(diff == 0, "chain fill (hint %u): %llu arena bytes differ", hints[h], (unsigned long long)diff);
         CHECK(bad == 0, "chain fill: d_bad = %u", bad);
     }
+    hipFree(d_arena); hipFree(d_foff); hipFree(d_flen); hipFree(d_first); hipFree(d_seed); hipFree(d_out);
+    hipFree(d_bad);
+    free(first); free(foff); free(flen); free(seed); free(want); free(got); free(arena); free(expect); free(after);
+    return 0;
+}
+
+/* rns_csum_chain_fill_dev with RNS_FLAG_CHAIN_TX_PACKED on the layout it streams: 20-byte
+ * heads back to back in a header region, each packet's payload (0..1480 bytes) one fragment,
+ * the payloads back to back at 16-byte-aligned starts after the header region (the
+ * transmit-rows kernel's row path). */
+static int test_chain_fill_txpacked(hipStream_t st)
+{
+    const uint32_t npk = 3000, hl = 20, fo = 16;
+    uint32_t *first = malloc((npk + 1) * sizeof *first);
+    uint64_t *foff = malloc(npk * 2 * sizeof *foff);
+    uint32_t *flen = malloc(npk * 2 * sizeof *flen);
+    uint16_t *seed = malloc(npk * sizeof *seed), *want = malloc(npk * sizeof *want), *got = malloc(npk * sizeof *got);
+    uint64_t pos = (((uint64_t)npk * hl + 4095) & ~4095ull);
+    uint32_t nf = 0;
+    for (uint32_t i = 0; i < npk; ++i) {
+        const uint64_t r = next_u64();
+        const uint32_t pl = (r % 7 == 0) ? 0u : (uint32_t)((r >> 8) % 1481u);
+        first[i] = nf;
+        seed[i] = (uint16_t)(r >> 32);
+        foff[nf] = (uint64_t)i * hl;
+        flen[nf++] = hl;
+        if (pl) {
+            foff[nf] = pos;
+            flen[nf++] = pl;
+            pos += (pl + 15u) & ~15u;
+        }
+    }
+    first[npk] = nf;
+    const uint64_t bytes = pos + 64;
+    uint8_t *arena = malloc(bytes), *expect = malloc(bytes), *after = malloc(bytes);
+    fill_random(arena, bytes);
+    memcpy(expect, arena, bytes);
+    for (uint32_t i = 0; i < npk; ++i)
+        expect[foff[first[i]] + fo] = expect[foff[first[i]] + fo + 1] = 0;
+    oracle_chain_batch(expect, foff, flen, first, seed, want, npk, 1);
+    for (uint32_t i = 0; i < npk; ++i) {
+        expect[foff[first[i]] + fo] = (uint8_t)(want[i] >> 8);
+        expect[foff[first[i]] + fo + 1] = (uint8_t)want[i];
+    }
+    uint8_t *d_arena;
+    uint64_t *d_foff;
+    uint32_t *d_flen, *d_first, *d_bad, bad = 1;
+    uint16_t *d_seed, *d_out;
+    HIP_OK(hipMalloc((void **)&d_arena, bytes));
+    HIP_OK(hipMalloc((void **)&d_foff, nf * sizeof *foff));
+    HIP_OK(hipMalloc((void **)&d_flen, nf * sizeof *flen));
+    HIP_OK(hipMalloc((void **)&d_first, (npk + 1) * sizeof *first));
+    HIP_OK(hipMalloc((void **)&d_seed, npk * sizeof *seed));
+    HIP_OK(hipMalloc((void **)&d_out, npk * sizeof *got));
+    HIP_OK(hipMalloc((void **)&d_bad, sizeof *d_bad));
+    HIP_OK(hipMemcpy(d_arena, arena, bytes, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_foff, foff, nf * sizeof *foff, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_flen, flen, nf * sizeof *flen, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_first, first, (npk + 1) * sizeof *first, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_seed, seed, npk * sizeof *seed, hipMemcpyHostToDevice));
+    HIP_OK(hipMemset(d_bad, 0, sizeof *d_bad));
+    CHECK(rns_csum_chain_fill_dev(d_arena, bytes, d_foff, d_flen, nf, d_first, d_seed, NULL, fo, d_out, npk,
+                                  RNS_FLAG_COMPLEMENT | RNS_FLAG_CHAIN_TX_PACKED, 750u, d_bad, st) == RNS_OK,
+          "rns_csum_chain_fill_dev (transmit-packed)");
+    HIP_OK(hipStreamSynchronize(st));
+    HIP_OK(hipMemcpy(got, d_out, npk * sizeof *got, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(after, d_arena, bytes, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(&bad, d_bad, sizeof bad, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < npk; ++i)
+        CHECK(got[i] == want[i], "transmit-packed chain fill packet %u: %04x != %04x", i, got[i], want[i]);
+    uint64_t diff = 0;
+    for (uint64_t b = 0; b < bytes; ++b)
+        diff += after[b] != expect[b];
+    CHECK(diff == 0, "transmit-packed chain fill: %llu arena bytes differ", (unsigned long long)diff);
+    CHECK(bad == 0, "transmit-packed chain fill: d_bad = %u", bad);
     hipFree(d_arena); hipFree(d_foff); hipFree(d_flen); hipFree(d_first); hipFree(d_seed); hipFree(d_out);
     hipFree(d_bad);
     free(first); free(foff); free(flen); free(seed); free(want); free(got); free(arena); free(expect); free(after);
@@ -557,7 +635,7 @@ int main(void)
 
     /* 2b. the packed entry bench.py times, the fragment-chain entry, transmit finalize and
      *     receive verify: each against the oracle's util.rs restatement */
-    if (test_packed(st) || test_strided(st) || test_chains(st) || test_chain_fill(st) || test_tx_rx(st))
+    if (test_packed(st) || test_strided(st) || test_chains(st) || test_chain_fill(st) || test_chain_fill_txpacked(st) || test_tx_rx(st))
         return 2;
 
     /* 3. errors come back as status codes, never as aborts */
