@@ -1,7 +1,7 @@
 // Per-XCD timing probe: does one XCD finish a streaming read later than the others?
 //
 //   hipcc --offload-arch=gfx950 -O3 tools/xcd_probe.hip -o tools/xcd_probe
-//   ./tools/xcd_probe [waves] [bytes_per_wave] [reps]
+//   ./tools/xcd_probe [waves] [bytes_per_wave] [reps] [shift]
 //
 // Each wave (one 64-lane workgroup) streams its own contiguous slice with 16-byte loads, 16 KiB
 // in flight (the rows kernel's D = 16), and records its XCD (HW_REG_XCC_ID), its first and last
@@ -28,12 +28,13 @@
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(64, 4) void stream_probe(const uint8_t *arena, uint64_t per_wave, uint64_t *rec,
-                                                      uint32_t *sink)
+                                                      uint32_t *sink, uint32_t shift)
 {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     // XCC_ID: hwreg 20, bits [3:0]
     const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
-    const uint8_t *base = arena + static_cast<uint64_t>(blockIdx.x) * per_wave;
+    // (shift: block b streams slice (b + shift) mod grid — does the slowness follow the XCD or the addresses?)
+    const uint8_t *base = arena + static_cast<uint64_t>((blockIdx.x + shift) % gridDim.x) * per_wave;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base), static_cast<short>(0),
                                                                       static_cast<int>(per_wave), 0x00020000);
     const uint32_t lane = threadIdx.x;
@@ -68,6 +69,7 @@ int main(int argc, char **argv)
     const uint32_t waves = argc > 1 ? static_cast<uint32_t>(std::atoi(argv[1])) : 4096u;
     const uint64_t per_wave = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 576ull << 10;
     const int reps = argc > 3 ? std::atoi(argv[3]) : 5;
+    const uint32_t shift = argc > 4 ? static_cast<uint32_t>(std::atoi(argv[4])) : 0u;
     const uint64_t bytes = per_wave * waves;
     uint8_t *arena;
     uint64_t *rec;
@@ -82,7 +84,7 @@ int main(int argc, char **argv)
         CHECK(hipEventCreate(&e0));
         CHECK(hipEventCreate(&e1));
         CHECK(hipEventRecord(e0, 0));
-        hipLaunchKernelGGL(stream_probe, dim3(waves), dim3(64), 0, 0, arena, per_wave, rec, sink);
+        hipLaunchKernelGGL(stream_probe, dim3(waves), dim3(64), 0, 0, arena, per_wave, rec, sink, shift);
         CHECK(hipGetLastError());
         CHECK(hipEventRecord(e1, 0));
         CHECK(hipEventSynchronize(e1));
@@ -105,8 +107,8 @@ int main(int argc, char **argv)
             s1[x] += b;
             m1[x] = std::max(m1[x], b);
         }
-        std::printf("{\"waves\": %u, \"bytes_per_wave\": %llu, \"event_us\": %.2f, \"span_us\": %.2f, \"GBps\": %.1f, \"xcd\": [",
-                    waves, static_cast<unsigned long long>(per_wave), ms * 1e3, (tmax - tmin) / 100.0, bytes / (ms * 1e6));
+        std::printf("{\"shift\": %u, \"waves\": %u, \"bytes_per_wave\": %llu, \"event_us\": %.2f, \"span_us\": %.2f, \"GBps\": %.1f, \"xcd\": [",
+                    shift, waves, static_cast<unsigned long long>(per_wave), ms * 1e3, (tmax - tmin) / 100.0, bytes / (ms * 1e6));
         bool first = true;
         for (int x = 0; x < 16; ++x) {
             if (cnt[x] == 0)
