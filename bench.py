@@ -107,8 +107,9 @@ def parse_args(argv=None):
     args = p.parse_args(argv)
     if args.shape and args.desc in ("32", "packed"):
         p.error("--shape overrides take 64-bit descriptors (--desc 64 or auto)")
-    if args.op == "verify" and (args.shape or args.desc not in ("auto", "64", "packed")):
-        p.error("--op verify takes the packed form (rns_rx_verify_packed_dev; auto) or 64-bit descriptors "
+    if args.op == "verify" and (args.shape or args.desc not in ("auto", "64", "packed", "strided")):
+        p.error("--op verify takes the packed form (rns_rx_verify_packed_dev), the strided form "
+                "(rns_rx_verify_strided_dev; auto for tiny datagrams in fixed-size slots) or 64-bit descriptors "
                 "(rns_rx_verify_dev) and the receive kernel's own shape")
     args.shard_rw = None
     if args.shard:
@@ -422,16 +423,21 @@ class GpuEngine:
         if op == "verify":  # packed receive arena (16-byte-aligned datagrams): the stream kernel; else 64-bit
             from rustnetworkstack_amd.workloads import make_verify_batch
             aligned = self.layout.n == 0 or int(self.layout.off[0]) % 16 == 0
-            form = "packed" if compact in ("auto", "packed") and aligned else "64"
+            # datagrams in fixed-size slots (c2's 64-byte ACKs): the strided receive entry, whose
+            # lanes load their datagrams beside their lengths (no block offset, no scan)
+            slots = self.layout.mean_len < 128 and self.batches[0].stride() is not None
+            form = ("strided" if (compact == "auto" and slots) or compact == "strided" else
+                    "packed" if compact in ("auto", "packed") and aligned else "64")
             for b in self.batches:
                 make_verify_batch(b)
-                if form == "packed":
+                if form in ("packed", "strided"):
                     b.launcher(packed=True)  # uploads blk_off / len16
         self.form = form
         self.compact = form == "32"
         self.packed = form == "packed"
         self.strided = form == "strided"
         self.verify_packed = op == "verify" and self.packed
+        self.verify_strided = op == "verify" and self.strided
         for b in self.batches:  # bind every rotating batch (and upload its descriptors) before any timing
             if op == "csum":
                 b.launcher(complement=True, shape=shape, compact=self.compact, packed=self.packed,
@@ -453,8 +459,13 @@ class GpuEngine:
         return self.layout.payload_bytes
 
     def _verify_call(self, b):
-        from rustnetworkstack_amd.batch import rx_verify, rx_verify_packed
+        from rustnetworkstack_amd.batch import rx_verify, rx_verify_packed, rx_verify_strided
         from rustnetworkstack_amd.workloads import LOCAL4, LOCAL6
+        if self.verify_strided:
+            if not hasattr(b, "slot_stride"):
+                b.slot_stride = b.stride()[:2]  # (first_off, stride), computed once per batch
+            first, stride = b.slot_stride
+            return lambda: rx_verify_strided(b.arena, stride, b.len16, LOCAL4, LOCAL6, first_off=first, status=b.status)
         if self.verify_packed:
             return lambda: rx_verify_packed(b.arena, b.blk_off, b.len16, LOCAL4, LOCAL6, status=b.status)
         return lambda: rx_verify(b.arena, b.off, b.length, LOCAL4, LOCAL6, status=b.status)  # current stream
@@ -565,6 +576,9 @@ class GpuEngine:
     def kernel_name(self) -> str:
         from rustnetworkstack_amd import _lib
         if self.op == "verify":
+            if self.verify_strided:
+                return ("csum_strided_rx_kernel (rns_rx_verify_strided_dev: datagrams in fixed-size slots; each lane "
+                        "loads its datagram's first 64 bytes beside its length, two 64-datagram batches per wave)")
             if self.verify_packed:
                 b = self.batches[0]
                 if (b.arena.numel() // max(self.layout.n, 1)) <= 128:
@@ -856,7 +870,7 @@ def main(argv=None):
     algo_bytes = engine.payload_bytes + (1 if verify else 2) * engine.n
     # descriptor bytes a launch reads (seeds included): packed 2 B length + 8 B per 64 packets
     desc_bytes = (engine.n * (2 + (0 if verify else 2)) + 8 * ((engine.n + 63) // 64) if engine.packed
-                  else 2 * engine.n if getattr(engine, "strided", False)  # the seeds only
+                  else 2 * engine.n if getattr(engine, "strided", False)  # the seeds (verify: the u16 lengths)
                   else engine.n * ((4 if engine.compact else 8) + 4 + (0 if verify else 2)))
     kernel_us = kernel_ms * 1e3
     achieved = algo_bytes / (kernel_us * 1e-6) / 1e9
@@ -893,7 +907,9 @@ def main(argv=None):
             "kernel_shape": list(shape) if shape else "auto",
             "descriptors": ({"64": "u64 offset + u32 length per datagram (rns_rx_verify_dev)",
                              "packed": "packed: u16 length per datagram, u64 offset per 64 datagrams "
-                                       "(rns_rx_verify_packed_dev)"} if verify else
+                                       "(rns_rx_verify_packed_dev)",
+                             "strided": "strided: u16 length per datagram, offsets implied by the slot stride "
+                                        "(rns_rx_verify_strided_dev)"} if verify else
                             {"32": "u32 offset + u32 length + u16 seed (rns_csum_batch_dev_off32)",
                              "64": "u64 offset + u32 length + u16 seed (rns_csum_batch_dev)",
                              "packed": "packed: u16 length + u16 seed per packet, u64 offset per 64 packets "

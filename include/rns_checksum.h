@@ -263,6 +263,18 @@ int rns_rx_verify_packed_dev(const uint8_t *d_arena, uint64_t arena_bytes, const
                              const uint16_t *d_len16, uint32_t align_log2, uint32_t n, const uint8_t *local_ipv4,
                              const uint8_t *local_ipv6, uint8_t *d_status, uint16_t *d_l4_sum, void *stream);
 
+/* Receive verify of datagrams at a FIXED STRIDE (a receive ring of fixed-size slots:
+ * the reference's 2048-byte MRU buffers, netif.rs:66, or 64-byte ACK slots): datagram i
+ * = d_arena[first_off + i * stride .. + d_len16[i]); per datagram exactly the checks and
+ * status bits of rns_rx_verify_dev (ip.rs:65-131, tcp.rs:838-850, icmp.rs:44-75).  No
+ * offsets travel and there is no per-block scan: with 16-byte-aligned slots every lane
+ * loads its datagram's first 64 bytes beside its length, so an ACK-sized datagram costs
+ * one memory round; longer datagrams are summed by a whole wave each.  Any stride and
+ * alignment is accepted (datagrams may even overlap: nothing is written to the arena). */
+int rns_rx_verify_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uint64_t first_off, uint64_t stride,
+                              const uint16_t *d_len16, uint32_t n, const uint8_t *local_ipv4, const uint8_t *local_ipv6,
+                              uint8_t *d_status, uint16_t *d_l4_sum, void *stream);
+
 /* Transmit finalize (SURVEY a6, §8f row 2 for whole datagrams): for each finished
  * outgoing IP datagram d_arena[d_off[i] .. + d_len[i]), the checksums the stack's
  * transmit path stores — tcp_output (tcp.rs:957-973: pseudo-header from the header's
@@ -278,6 +290,18 @@ int rns_rx_verify_packed_dev(const uint8_t *d_arena, uint64_t arena_bytes, const
 #define RNS_TX_MALFORMED      0x80u  /* bad version / IHL / too short, or outside the arena: untouched */
 int rns_tx_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off, const uint32_t *d_len,
                     uint32_t n, uint8_t *d_status, void *stream);
+
+/* Transmit finalize of a PACKED transmit arena (the descriptor form of
+ * rns_csum_batch_packed_dev: u16 lengths, d_blk_off[b] = offset of datagram 64*b, datagrams
+ * back to back at 2^align_log2 boundaries, align_log2 >= 4): per datagram exactly what
+ * rns_tx_fill_dev stores and reports (tcp.rs:957-973, udp.rs:151-171, icmp.rs:87-112,
+ * ip.rs:140-160; both fields computed as zero, pseudo-headers from the header's own
+ * addresses).  One wave streams each 64-datagram block as whole 1 KiB rows (the rows kernel)
+ * while each owner holds its datagram's header chunks and stores its two fields with one
+ * 2-byte store each.  len_hint = the typical datagram length (row depth; 0 = unknown).
+ * d_status optional.  align_log2 < 4 is RNS_E_INVALID. */
+int rns_tx_fill_packed_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_blk_off, const uint16_t *d_len16,
+                           uint32_t align_log2, uint32_t n, uint8_t *d_status, uint32_t len_hint, void *stream);
 
 /* Tuning entry (bench / tests): explicit kernel shape.  variant bit 0: 0 = group
  * kernel (one lane stores each result), 1 = rounds kernel (a wave owns 64

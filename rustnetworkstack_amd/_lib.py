@@ -56,7 +56,9 @@ EXPORTED_SYMBOLS = (
     "rns_csum_fill_packed_dev",
     "rns_rx_verify_dev",
     "rns_rx_verify_packed_dev",
+    "rns_rx_verify_strided_dev",
     "rns_tx_fill_dev",
+    "rns_tx_fill_packed_dev",
     "rns_host_ctx_create",
     "rns_host_ctx_destroy",
     "rns_csum_batch_host",
@@ -130,7 +132,9 @@ _SIGNATURES = {
     "rns_csum_fill_packed_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp, _u32, _vp, _u32, _u32, _u32, _vp, _vp]),
     "rns_rx_verify_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),
     "rns_rx_verify_packed_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp]),
+    "rns_rx_verify_strided_dev": (_int, [_vp, _u64, _u64, _u64, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),
     "rns_tx_fill_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp]),
+    "rns_tx_fill_packed_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _u32, _vp, _u32, _vp]),
     "rns_host_ctx_create": (_int, [_int, _u64, _u32, ctypes.POINTER(_vp)]),
     "rns_host_ctx_destroy": (_int, [_vp]),
     "rns_csum_batch_host": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32]),

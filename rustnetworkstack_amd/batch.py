@@ -535,6 +535,65 @@ def rx_verify_packed(arena: torch.Tensor, blk_off: torch.Tensor, len16: torch.Te
     return status
 
 
+def rx_verify_strided(arena: torch.Tensor, stride: int, len16: torch.Tensor, local_ipv4: bytes, local_ipv6: bytes,
+                      *, first_off: int = 0, status: torch.Tensor | None = None,
+                      l4_sum: torch.Tensor | None = None) -> torch.Tensor:
+    """Receive verify of datagrams at a fixed stride (rns_rx_verify_strided_dev): datagram i
+    = ``arena[first_off + i*stride : + len16[i]]``, a ring of fixed-size receive slots.  The
+    same uint8 status per datagram as rx_verify."""
+    _require_cuda(arena, "arena", (torch.uint8,))
+    _require_cuda(len16, "len16", _U16)
+    if len(local_ipv4) != 4 or len(local_ipv6) != 16:
+        raise ValueError("local_ipv4 must be 4 bytes and local_ipv6 16 bytes")
+    if not (0 <= int(first_off) < 2 ** 64 and 0 <= int(stride) < 2 ** 64):
+        raise ValueError("first_off and stride must be u64")
+    n = len16.numel()
+    if n >= 2 ** 32:
+        raise ValueError("at most 2^32-1 datagrams per call")
+    dev = arena.device
+    lib = _lib.load()
+    status, l4_ptr = _rx_outputs(dev, n, status, l4_sum, (("len16", len16),))
+    with torch.cuda.device(dev):
+        st = lib.rns_rx_verify_strided_dev(arena.data_ptr(), arena.numel(), int(first_off), int(stride),
+                                           len16.data_ptr(), n, bytes(local_ipv4), bytes(local_ipv6),
+                                           status.data_ptr(), l4_ptr, _stream_handle(dev))
+    _lib.check(st, "rns_rx_verify_strided_dev")
+    return status
+
+
+def tx_fill_packed(arena: torch.Tensor, blk_off: torch.Tensor, len16: torch.Tensor, *, align_log2: int = 4,
+                   status: torch.Tensor | None = None, len_hint: int = 0) -> torch.Tensor:
+    """Transmit finalize of a PACKED arena of outgoing datagrams (rns_tx_fill_packed_dev: u16
+    lengths, one offset per 64 datagrams, starts at 2^align_log2 boundaries, align_log2 >= 4):
+    the bytes and the uint8 status per datagram of ``tx_fill``."""
+    _require_cuda(arena, "arena", (torch.uint8,))
+    _require_cuda(blk_off, "blk_off", (torch.int64,))
+    _require_cuda(len16, "len16", _U16)
+    n = len16.numel()
+    if blk_off.numel() < (n + 63) // 64:
+        raise ValueError("blk_off needs one offset per 64 datagrams")
+    if not 4 <= align_log2 <= 12:
+        raise ValueError("the packed transmit finalize needs align_log2 in 4..12")
+    if n >= 2 ** 32:
+        raise ValueError("at most 2^32-1 datagrams per call")
+    dev = arena.device
+    for name, t in (("blk_off", blk_off), ("len16", len16)):
+        if t.device != dev:
+            raise ValueError(f"{name} is on {t.device}, arena on {dev}")
+    if status is None:
+        status = torch.empty(n, dtype=torch.uint8, device=dev)
+    else:
+        _require_cuda(status, "status", (torch.uint8,))
+        if status.numel() != n or status.device != dev:
+            raise ValueError(f"status must be {n} uint8 entries on {dev}")
+    with torch.cuda.device(dev):
+        st = _lib.load().rns_tx_fill_packed_dev(arena.data_ptr(), arena.numel(), blk_off.data_ptr(),
+                                               len16.data_ptr(), int(align_log2), n, status.data_ptr(),
+                                               int(len_hint), _stream_handle(dev))
+    _lib.check(st, "rns_tx_fill_packed_dev")
+    return status
+
+
 def tx_fill(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, *,
             status: torch.Tensor | None = None) -> torch.Tensor:
     """Transmit finalize of a batch of outgoing IP datagrams (rns_tx_fill_dev): the

@@ -117,4 +117,40 @@ int launch_fill_packed(const CsumArgs &a, hipStream_t st)
     return hip_status(hipGetLastError());
 }
 
+// Transmit finalize of a packed arena (align_log2 >= 4): the rows transmit kernel, D by the
+// typical length as for the plain checksum.
+#ifndef RNS_TX_ROWS_DEEP_FROM  // typical lengths from this take D = 16 rows at 4 waves/SIMD
+#define RNS_TX_ROWS_DEEP_FROM 1024u
+#endif
+int launch_tx_packed(const CsumArgs &a, hipStream_t st)
+{
+    constexpr bool NT = RNS_STREAM_NT != 0;
+    const bool buf = buf_records(a) < kOobOffset;
+    const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);
+    if (a.len_hint >= RNS_TX_ROWS_DEEP_FROM) {
+        if (buf)
+            hipLaunchKernelGGL((csum_rows_tx_kernel<NT, true, 16>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_rows_tx_kernel<NT, false, 16>), grid, block, 0, st, a);
+    } else {
+        if (buf)
+            hipLaunchKernelGGL((csum_rows_tx_kernel<NT, true, 8>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((csum_rows_tx_kernel<NT, false, 8>), grid, block, 0, st, a);
+    }
+    return hip_status(hipGetLastError());
+}
+
+// Receive verify of datagrams at a fixed stride: B batches of 64 per one-wave workgroup.
+int launch_strided_rx(const CsumArgs &a, hipStream_t st)
+{
+    constexpr int B = RNS_STRIDED_RX_B;
+    const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 64 * B - 1) / (64 * B))), block(64);
+    if (buf_records(a) < kOobOffset)
+        hipLaunchKernelGGL((csum_strided_rx_kernel<true, B>), grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL((csum_strided_rx_kernel<false, B>), grid, block, 0, st, a);
+    return hip_status(hipGetLastError());
+}
+
 }  // namespace rns

@@ -431,6 +431,51 @@ int rns_rx_verify_packed_dev(const uint8_t *d_arena, uint64_t arena_bytes, const
     return launch_stream_rx(a, static_cast<hipStream_t>(stream));
 }
 
+int rns_rx_verify_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uint64_t first_off, uint64_t stride,
+                              const uint16_t *d_len16, uint32_t n, const uint8_t *local_ipv4, const uint8_t *local_ipv6,
+                              uint8_t *d_status, uint16_t *d_l4_sum, void *stream)
+{
+    if (n == 0)
+        return RNS_OK;
+    if (!d_arena || !d_len16 || !d_status || !local_ipv4 || !local_ipv6)
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    CsumArgs a{};
+    set_arena(a, d_arena, arena_bytes);
+    a.len16 = d_len16;
+    a.first_off = first_off;
+    a.stride = stride;
+    a.n = n;
+    a.flags = RNS_FLAG_COMPLEMENT;
+    a.status = d_status;
+    a.l4_out = d_l4_sum;
+    a.local4_sum = be_sum(local_ipv4, 4);
+    a.local6_sum = be_sum(local_ipv6, 16);
+    return launch_strided_rx(a, static_cast<hipStream_t>(stream));
+}
+
+int rns_tx_fill_packed_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_blk_off, const uint16_t *d_len16,
+                           uint32_t align_log2, uint32_t n, uint8_t *d_status, uint32_t len_hint, void *stream)
+{
+    if (n == 0)
+        return RNS_OK;
+    if (!d_arena || !d_blk_off || !d_len16 || align_log2 < 4 || align_log2 > 12)
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    CsumArgs a{};
+    set_arena(a, d_arena, arena_bytes);
+    a.len16 = d_len16;
+    a.blk_off = d_blk_off;
+    a.align_mask = (1u << align_log2) - 1u;
+    a.n = n;
+    a.flags = RNS_FLAG_COMPLEMENT;
+    a.status = d_status;
+    a.len_hint = len_hint;
+    return launch_tx_packed(a, static_cast<hipStream_t>(stream));
+}
+
 int rns_tx_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off, const uint32_t *d_len,
                     uint32_t n, uint8_t *d_status, void *stream)
 {

@@ -428,6 +428,386 @@ __global__ __launch_bounds__(64, RNS_ROWS_RX_OCC) void csum_rows_rx_kernel(const
 }
 
 // ---------------------------------------------------------------------------
+// Receive verify of datagrams at a fixed stride (rns_rx_verify_strided_dev, round 6):
+// datagram i = arena[first_off + i * stride, + len16[i]) — a receive ring of fixed-size slots
+// (64-byte ACK slots, or the reference's 2048-byte MRU buffers, netif.rs:66).  No block offsets
+// and no scan: every lane computes its datagram's address itself, so with 16-byte-aligned
+// slots its first 4 chunks (64 bytes) are loaded together with its length — one memory latency
+// for the descriptors and the bytes of an ACK-sized datagram, where the packed form's ACK path
+// waits for the block offset, scans the lengths, and only then loads (the prologue the strided
+// tiny kernel took off the 64-byte checksum).  A datagram longer than 64 bytes is summed by
+// the whole wave, one datagram at a time (as the packed kernels' unaligned path); its header
+// is in the same 4 chunks.  Unaligned slots take that loop for every datagram and load their
+// header chunks from the 16-byte boundary below the start.  B 64-datagram batches per wave.
+// ---------------------------------------------------------------------------
+#ifndef RNS_STRIDED_RX_B  // 64-datagram batches per wave of the strided receive kernel
+#define RNS_STRIDED_RX_B 2
+#endif
+#ifndef RNS_STRIDED_RX_AUX  // cache-policy bits of its slot loads (A/B)
+#define RNS_STRIDED_RX_AUX 0
+#endif
+template <bool BUF, int B>
+__global__ __launch_bounds__(64) void csum_strided_rx_kernel(const CsumArgs a)
+{
+    const uint32_t lane = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
+    const uint64_t recs = buf_records(a);
+    const uint64_t start0 = a.first_off + a.base_adjust;
+    const bool aligned = ((start0 | a.stride) & 15) == 0;  // uniform: a kernel argument
+    uint32_t len[B];
+    uint64_t st[B];
+    uint4 own[B][4];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const uint64_t p = (static_cast<uint64_t>(blockIdx.x) * B + b) * 64 + lane;
+        const bool live = p < a.n;
+        len[b] = live ? static_cast<uint32_t>(a.len16[live ? p : a.n - 1]) : 0u;
+        st[b] = start0 + p * a.stride;
+        // chunks 0-3 of the slot, issued beside the length (zero past the arena; bytes past the
+        // datagram are masked once its length is known)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t o = st[b] + 16u * i;
+            const bool in = aligned && live && o + 16 <= recs && st[b] <= a.arena_bytes;
+            if constexpr (BUF) {
+                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, in ? static_cast<uint32_t>(o) : kOobOffset,
+                                                                      0, RNS_STRIDED_RX_AUX);
+                own[b][i] = make_uint4(x.x, x.y, x.z, x.w);
+            } else {
+                const uint4 x = load_chunk<false>(a.arena + (in ? o : 0));
+                own[b][i] = in ? x : make_uint4(0, 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const uint64_t p = (static_cast<uint64_t>(blockIdx.x) * B + b) * 64 + lane;
+        const bool live = p < a.n;
+        const uint32_t L = len[b];
+        const uint64_t start = st[b];
+        const bool ok = start <= a.arena_bytes && L <= a.arena_bytes - start;
+        const bool present = live && ok && L != 0;
+        uint32_t mine = 0;
+        uint4 hd[5];
+        hd[4] = make_uint4(0, 0, 0, 0);
+        if (aligned) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uint4 x = own[b][i];
+                if (16u * i + 16u > L)  // an ACK-sized datagram's bytes past its end never count
+                    x = 16u * i < L ? keep_first(x, L - 16u * i) : make_uint4(0, 0, 0, 0);
+                hd[i] = x;
+                mine = __builtin_amdgcn_sad_u16(x.x, 0, mine);
+                mine = __builtin_amdgcn_sad_u16(x.y, 0, mine);
+                mine = __builtin_amdgcn_sad_u16(x.z, 0, mine);
+                mine = __builtin_amdgcn_sad_u16(x.w, 0, mine);
+            }
+        }
+        uint64_t todo = __ballot(present && (!aligned || L > 64));
+        if (todo) {
+            // ---- longer (or unaligned) datagrams: the whole wave sums one at a time ----
+            while (todo) {
+                const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
+                todo &= todo - 1;
+                const uint64_t sto =
+                    (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start >> 32), o)))
+                     << 32) |
+                    static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start), o));
+                const uint32_t Lo = __builtin_amdgcn_readlane(L, o);
+                const Pkt k = make_pkt(sto, Lo);
+                uint32_t acc = 0;
+                for (uint32_t cc = 0; cc < k.nch; cc += 64) {
+                    uint4 w[1];
+                    issue_pass<64, 1, true, BUF, 1>(a, rsrc, k, cc + lane, w);
+                    mask_edges<64, 1, 1>(k, cc + lane, w);
+                    acc = sum_le<1, 1>(w, acc);
+                }
+                const uint32_t sum = group_allreduce<64>(acc);
+                mine = lane == o ? sum : mine;
+            }
+        }
+        uint8_t stv;
+        uint32_t l4_res = 0;
+        if (aligned) {
+            stv = rx_finish<4>(a, hd, mine, 0u, L, false, false, present, l4_res);
+        } else {
+            // the header from the 16-byte boundary below the start: 5 chunks hold its first
+            // 65-80 bytes, masked to the datagram
+            const uint64_t b0 = start & ~15ull;
+            const uint32_t s0 = static_cast<uint32_t>(start & 15);
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                hd[i] = own_chunk<BUF>(a, rsrc, recs, b0, present ? s0 + L : 0u, i);
+                const int lo = static_cast<int>(s0) - 16 * i, hi = static_cast<int>(s0 + L) - 16 * i;
+                hd[i] = make_uint4(keep_bytes(hd[i].x, lo, hi, 0), keep_bytes(hd[i].y, lo, hi, 4),
+                                   keep_bytes(hd[i].z, lo, hi, 8), keep_bytes(hd[i].w, lo, hi, 12));
+            }
+            stv = rx_finish<5>(a, hd, mine, s0, L, start & 1, false, present, l4_res);
+        }
+        if (live) {
+            a.status[p] = stv;
+            if (a.l4_out)
+                a.l4_out[p] = static_cast<uint16_t>(l4_res);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Transmit finalize through the rows decomposition (rns_tx_fill_packed_dev, round 6):
+// tcp_output (tcp.rs:957-973), udp_output (udp.rs:151-171), icmp_output_v4/v6
+// (icmp.rs:87-112) and ip_output_v4 (ip.rs:140-160) over a packed arena of finished
+// datagrams.  The datagram's word sum T comes from the rows as in csum_rows_rx_kernel, and
+// its owner holds the first 3 chunks (loaded a group of rows ahead of the row that streams
+// them) — the IPv4 header without options, both fields of an IPv4 datagram, both addresses
+// of either family; chunks 3-4 are loaded only by the owners that need them (IPv4 options,
+// TCP over IPv6).  The owner parses the header, takes the header sum H and the two fields'
+// bytes out of T (both fields count as zero: buf.rs:286-288), forms the pseudo-header from
+// the header's own addresses and stores each result with one 2-byte store (two-byte stores
+// measured no dearer than sector rewrites: profiles/r04_fill_store_ab.json).  The stash
+// kernel this replaces needed a class pass, an LDS stash and two 32-byte sector rewrites.
+// ---------------------------------------------------------------------------
+#ifndef RNS_ROWS_TX_OCC  // waves/SIMD bound of the transmit form
+#define RNS_ROWS_TX_OCC 6
+#endif
+constexpr uint32_t kNoField = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t bswap16_u32(uint32_t x) { return ((x & 0xff) << 8) | (x >> 8); }
+
+// Two big-endian 16-bit words of a dword held little-endian (bytes b0 b1 b2 b3): b0b1 + b2b3.
+__device__ __forceinline__ uint32_t be2(uint32_t d)
+{
+    const uint32_t x = ((d & 0x00ff00ffu) << 8) | ((d >> 8) & 0x00ff00ffu);
+    return (x & 0xffffu) + (x >> 16);
+}
+
+// The first 40 bytes of a datagram (version, IHL, protocol and both addresses of either
+// family) as ten dwords in datagram byte order, from its chunks (s = start & 15; chunk 0 is
+// the 16-byte boundary at or below the start; s > 0 needs NS >= 4).
+template <int NS>
+__device__ __forceinline__ void head40(const uint4 (&ch)[NS], uint32_t s, uint32_t (&h)[10])
+{
+    uint32_t w[4 * NS];
+#pragma unroll
+    for (int c = 0; c < NS; ++c) {
+        w[4 * c] = ch[c].x;
+        w[4 * c + 1] = ch[c].y;
+        w[4 * c + 2] = ch[c].z;
+        w[4 * c + 3] = ch[c].w;
+    }
+    if (s == 0) {
+#pragma unroll
+        for (int k = 0; k < 10; ++k)
+            h[k] = w[k];
+        return;
+    }
+    if constexpr (NS >= 4) {
+        const uint32_t q = s >> 2, sh = s & 3;
+        uint32_t d[11];
+#pragma unroll
+        for (int k = 0; k < 11; ++k)
+            d[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
+#pragma unroll
+        for (int k = 0; k < 10; ++k)
+            h[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+    }
+}
+
+// Owner-lane finish of transmit finalize for one datagram of L bytes: ch = its chunks from
+// the 16-byte boundary at or below its start (raw memory bytes; s = start & 15; NS chunks
+// hold bytes up to s + 78: the TCP field behind a 60-byte IPv4 header), mine = the
+// datagram's word sum T (LE words at absolute pairing; L <= 65535, so no u32 wrap), odd =
+// start & 1.  Exactly the stash kernel's transmit finish (csum_mixed_kernel, TX mode) and
+// oracle.tx_fill_ref: fld[0] = 10 for IPv4 (ip_output_v4 over IHL*4 bytes), fld[1] = the
+// L4 field (TCP 16, UDP 6, ICMPv4 / ICMPv6 2, after the IP header) when the segment holds
+// it; val[] = the values to store big-endian (complemented; UDP's 0 stored as is).
+template <int NS>
+__device__ __forceinline__ uint8_t tx_finish(const uint4 (&ch)[NS], uint32_t mine, uint32_t s, uint32_t L, bool odd,
+                                             bool present, uint32_t (&fld)[2], uint32_t (&val)[2])
+{
+    fld[0] = fld[1] = kNoField;
+    val[0] = val[1] = 0;
+    if (!present)
+        return RNS_TX_MALFORMED;
+    uint32_t h[10];
+    head40(ch, s, h);
+    const uint32_t b0 = h[0] & 0xffu, version = b0 >> 4;
+    uint32_t hdr, proto, addr;  // addr: BE word sum of source + destination (tcp.rs:958-966)
+    if (version == 4) {
+        hdr = (b0 & 15u) * 4u;
+        if (hdr < 20 || hdr > L)
+            return RNS_TX_MALFORMED;
+        proto = (h[2] >> 8) & 0xffu;            // header[9]
+        addr = be2(h[3]) + be2(h[4]);            // header[12..20]
+    } else if (version == 6) {
+        hdr = 40;
+        if (L < 40)
+            return RNS_TX_MALFORMED;
+        proto = (h[1] >> 16) & 0xffu;           // header[6]
+        addr = 0;
+#pragma unroll
+        for (int k = 2; k < 10; ++k)             // header[8..40]
+            addr += be2(h[k]);
+    } else {
+        return RNS_TX_MALFORMED;
+    }
+    const uint32_t seg = L - hdr, l16 = seg & 0xffffu;  // packet.len() as u16 (tcp.rs:942, udp.rs:152)
+    uint32_t field = kNoField, seed = 0;
+    if (proto == 6 || proto == 17) {
+        field = proto == 6 ? 16u : 6u;
+        seed = fold16(addr + proto + l16);
+    } else if (proto == 1 && version == 4) {
+        field = 2;  // icmp_output_v4: no pseudo-header
+    } else if (proto == 58 && version == 6) {
+        field = 2;  // icmp_output_v6: full length, protocol 58
+        seed = fold16(addr + 58 + (seg >> 16) + (seg & 0xffffu));
+    }
+    const int lo = static_cast<int>(s);
+    const uint32_t H = stash_sum_le(ch, lo, lo + static_cast<int>(hdr));
+    uint8_t st = 0;
+    if (version == 4) {  // compute_checksum(header) with header[10..12] as zero
+        fld[0] = 10;
+        val[0] = finalize_bits(H - stash_sum_le(ch, lo + 10, lo + 12), odd, false, 0u, true, RNS_FLAG_COMPLEMENT);
+        st |= RNS_TX_IP_FILLED;
+    }
+    if (field != kNoField && seg >= field + 2) {
+        const uint32_t f = hdr + field;
+        fld[1] = f;
+        const uint32_t l4 = mine - H - stash_sum_le(ch, lo + static_cast<int>(f), lo + static_cast<int>(f) + 2);
+        val[1] = finalize_bits(l4, odd, false, seed, true, RNS_FLAG_COMPLEMENT);
+        st |= RNS_TX_L4_FILLED;
+    }
+    return st;
+}
+
+// set_be16 of a finished field at absolute arena offset fp (util.rs:132-135)
+template <bool BUF>
+__device__ __forceinline__ void store_field(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint64_t fp, uint32_t v)
+{
+    uint8_t *w8 = const_cast<uint8_t *>(a.arena);
+    if (fp & 1) {
+        w8[fp] = static_cast<uint8_t>(v >> 8);
+        w8[fp + 1] = static_cast<uint8_t>(v);
+    } else if constexpr (BUF) {
+        __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(bswap16_u32(v & 0xffffu)), rsrc,
+                                              static_cast<uint32_t>(fp), 0, 0);
+    } else {
+        *reinterpret_cast<uint16_t *>(w8 + fp) = static_cast<uint16_t>(bswap16_u32(v & 0xffffu));
+    }
+}
+
+template <bool NT, bool BUF, int D>
+__global__ __launch_bounds__(64, D >= 16 ? 4 : RNS_ROWS_TX_OCC) void csum_rows_tx_kernel(const CsumArgs a)
+{
+    constexpr int kNS = 5;  // chunks 0-4: bytes 0..79 of a 16-byte-aligned datagram
+    const uint32_t lane = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
+    const uint64_t recs = buf_records(a);
+    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * 64;
+    const uint64_t p = base + lane;
+    const bool live = p < a.n;
+    const uint64_t q = live ? p : a.n - 1;  // branch-free descriptor loads
+    const uint32_t zero_v = __builtin_amdgcn_mbcnt_lo(0u, 0u);
+    const uint64_t r0v = a.blk_off[(base >> 6) + zero_v];
+    const uint32_t len = live ? static_cast<uint32_t>(a.len16[q]) : 0u;
+    const uint64_t r0 =
+        ((static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(r0v >> 32))))
+          << 32) |
+         static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(r0v)))) +
+        a.base_adjust;  // the wave's first datagram
+    const uint32_t pad = (len + a.align_mask) & ~a.align_mask;
+    const uint32_t incl = wave_incl_scan(pad);
+    const uint32_t excl = incl - pad;
+    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);  // the region's bytes
+    const uint64_t start = r0 + excl;
+    const bool ok = start <= a.arena_bytes && len <= a.arena_bytes - start;
+    const bool present = live && ok && len != 0;
+    uint32_t mine = 0;
+    uint8_t st = RNS_TX_MALFORMED;
+    uint32_t fld[2], val[2];
+    // the bytes a datagram's finish reads past chunk 2 (from its first chunk): IPv4 options
+    // past byte 48, or an L4 field ending past it (TCP over IPv6, TCP / UDP behind options)
+    auto need_bytes = [&](const uint4 c0) -> uint32_t {
+        const uint32_t b0 = c0.x & 0xffu, v = b0 >> 4;
+        const uint32_t proto = v == 4 ? (c0.z >> 8) & 0xffu : (c0.y >> 16) & 0xffu;
+        const uint32_t hdr = v == 4 ? (b0 & 15u) * 4u : 40u;
+        const uint32_t fend = hdr + (proto == 6 ? 18u : proto == 17 ? 8u : 4u);
+        return v == 4 || v == 6 ? max(hdr, fend) : 0u;
+    };
+    if ((r0 & 15) == 0) {
+        uint4 own[kNS];
+        own[3] = own[4] = make_uint4(0, 0, 0, 0);
+        if (!__ballot(len > 64)) {
+            // ---- ACK-sized unit: every owner takes its datagram whole ----
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                own[i] = own_chunk<BUF>(a, rsrc, recs, start, len, i);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uint4 x = own[i];
+                if (16u * i + 16u > len)  // the sum sees none of the bytes past the end
+                    x = 16u * i < len ? keep_first(x, len - 16u * i) : make_uint4(0, 0, 0, 0);
+                mine = __builtin_amdgcn_sad_u16(x.x, 0, mine);
+                mine = __builtin_amdgcn_sad_u16(x.y, 0, mine);
+                mine = __builtin_amdgcn_sad_u16(x.z, 0, mine);
+                mine = __builtin_amdgcn_sad_u16(x.w, 0, mine);
+            }
+        } else {
+            // ---- the rows: T, and the owner's first 3 chunks loaded a group ahead ----
+            const uint32_t c0 = excl >> 4;
+            const uint32_t e = len ? (excl + len - 1) >> 4 : c0;
+            mine = rows_region_sum<NT, BUF, D, 3>(a, rsrc, recs, r0, total, c0, e, len, own);
+            const uint32_t nb = present ? need_bytes(own[0]) : 0u;
+            if (__ballot(nb > 48)) {
+                own[3] = nb > 48 ? own_chunk<BUF>(a, rsrc, recs, start, len, 3) : make_uint4(0, 0, 0, 0);
+                own[4] = nb > 64 ? own_chunk<BUF>(a, rsrc, recs, start, len, 4) : make_uint4(0, 0, 0, 0);
+            }
+        }
+        st = tx_finish<kNS>(own, mine, 0u, len, false, present, fld, val);
+    } else {
+        // ---- unaligned region (rare): the whole wave sums one datagram at a time ----
+        uint64_t todo = __ballot(present);
+        while (todo) {
+            const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
+            todo &= todo - 1;
+            const uint64_t sto =
+                (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start >> 32), o)))
+                 << 32) |
+                static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start), o));
+            const uint32_t L = __builtin_amdgcn_readlane(len, o);
+            const Pkt k = make_pkt(sto, L);
+            uint32_t acc = 0;
+            for (uint32_t cc = 0; cc < k.nch; cc += 64) {
+                uint4 w[1];
+                issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, w);
+                mask_edges<64, 1, 1>(k, cc + lane, w);
+                acc = sum_le<1, 1>(w, acc);
+            }
+            const uint32_t sum = group_allreduce<64>(acc);
+            mine = lane == o ? sum : mine;
+        }
+        // each owner takes chunks 0-5 from the 16-byte boundary below its start (its first
+        // 81-96 bytes)
+        const uint64_t b0 = start & ~15ull;
+        const uint32_t s0 = static_cast<uint32_t>(start & 15);
+        uint4 own[kNS + 1];
+#pragma unroll
+        for (int i = 0; i < kNS + 1; ++i)
+            own[i] = own_chunk<BUF>(a, rsrc, recs, b0, present ? s0 + len : 0u, i);
+        st = tx_finish<kNS + 1>(own, mine, s0, len, start & 1, present, fld, val);
+    }
+    // (after the wave's loads: a store between a load and its use would join the in-order
+    // vmcnt queue)
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        if (fld[k] != kNoField)
+            store_field<BUF>(a, rsrc, start + fld[k], val[k]);
+    if (live && a.status)
+        a.status[p] = st;
+}
+
+// ---------------------------------------------------------------------------
 // Transmit-shaped chains (RNS_FLAG_CHAIN_TX_PACKED; rns_csum_chain_dev and
 // rns_csum_chain_fill_dev).  What tcp_output checksums (tcp.rs:938-973) is a head fragment
 // (the TCP header alloc_header prepended, buf.rs:262-291) followed by the payload.  A batching
@@ -455,8 +835,6 @@ __global__ __launch_bounds__(64, RNS_ROWS_RX_OCC) void csum_rows_rx_kernel(const
 #define RNS_TXROWS_OCC 5  // (zero scratch at 86-89 VGPRs; 6 spills 32-116 B/lane)
 #endif
 constexpr uint32_t kTxHeadMax = 64;  // (head start & 15) + head length: at most 4 chunks
-
-__device__ __forceinline__ uint32_t bswap16_u32(uint32_t x) { return ((x & 0xff) << 8) | (x >> 8); }
 
 template <bool NT, bool BUF, int D, bool FILL>
 __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const CsumArgs a)

@@ -75,6 +75,8 @@ int launch_strided_tiny(const CsumArgs &a, hipStream_t st);
 int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st);
 int launch_fill_packed(const CsumArgs &a, hipStream_t st);
 int launch_stream_rx(const CsumArgs &a, hipStream_t st);
+int launch_tx_packed(const CsumArgs &a, hipStream_t st);
+int launch_strided_rx(const CsumArgs &a, hipStream_t st);
 // k_chain.hip: K packets per lane (1..kChainMaxK); FILL = the head-fragment fill
 template <bool FILL>
 int launch_chain(const CsumArgs &a, uint32_t K, bool nt, bool runs, hipStream_t st);

@@ -302,3 +302,79 @@ def test_output_buffers_are_checked():
         rx_verify_packed(arena, blk, len16, L4, L6, l4_sum=torch.empty(63, dtype=torch.uint16, device=DEV))
     st = rx_verify_packed(arena, blk, len16, L4, L6, status=torch.empty(64, dtype=torch.uint8, device=DEV))
     assert st.numel() == 64
+
+
+# --- receive rings of fixed-size slots (rns_rx_verify_strided_dev) -------------------------
+def run_strided_rx(pkts, stride, first_off, base_shift=0):
+    from rustnetworkstack_amd.batch import rx_verify_strided
+    n = len(pkts)
+    ln = np.array([len(p) for p in pkts], dtype=np.uint16)
+    arena = np.full(first_off + n * stride + 64 + base_shift, 0xA5, dtype=np.uint8)  # slot tails never count
+    for i, p in enumerate(pkts):
+        o = base_shift + first_off + i * stride
+        arena[o:o + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    big = torch.from_numpy(arena).to(DEV)
+    l4 = torch.empty(n, dtype=torch.uint16, device=DEV)
+    st = rx_verify_strided(big[base_shift:], stride, dev(ln, np.int16), L4, L6, first_off=first_off, l4_sum=l4)
+    return st.cpu().numpy(), l4.view(torch.int16).cpu().numpy().view(np.uint16)
+
+
+@pytest.mark.parametrize("stride,first_off,base_shift", [(2048, 0, 0), (2048, 48, 0), (2051, 0, 0), (2048, 5, 0),
+                                                         (2048, 0, 7), (1504, 16, 0)])
+def test_strided_mixed_datagrams_match_reference_path(oracle, stride, first_off, base_shift):
+    """Every kind of datagram in MRU-sized receive slots (netif.rs:66): 16-byte-aligned slots
+    (ACK-sized datagrams from the owners' loads, longer ones summed by the wave), and
+    unaligned strides, first offsets and arena bases (every datagram through the wave loop,
+    header chunks from the boundary below).  Status and L4 sum against the reference."""
+    pkts = make_packets(5000, 0x57D + stride + first_off + base_shift)
+    expect = [O.rx_verify_ref(p, L4, L6, ones_comp=oracle.compute_ones_comp) for p in pkts]
+    st, l4 = run_strided_rx(pkts, stride, first_off, base_shift)
+    got = list(zip(st.tolist(), l4.tolist()))
+    bad = [(i, len(pkts[i]), got[i], expect[i]) for i in range(len(pkts)) if got[i] != tuple(expect[i])]
+    assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("stride", [64, 80, 128])
+def test_strided_ack_slots_edge_datagrams(oracle, stride):
+    """ACK-sized slots: every IHL with short and empty segments, header-only UDP, one-byte
+    ICMP, short IPv6, garbage and empty datagrams; each slot's bytes past its datagram hold
+    0xA5 (never counted).  Datagrams longer than the slot overlap the next slot (read only)."""
+    pkts = []
+    for ihl in range(5, 16):
+        for size in (0, 1, 2, 3, 17, 31):
+            p = ipv4(6, tcp_seg(R4, L4, b"\x5a" * size), ihl=ihl)
+            pkts.append(p[:stride])
+        pkts.append(ipv4(6, b"", ihl=ihl))
+        pkts.append(ipv4(17, b"", ihl=ihl))
+        pkts.append(ipv4(1, b"\x00", ihl=ihl))
+    pkts += [ipv6(6, b""), ipv6(58, b"\x01"), ipv6(6, tcp_seg(R6, L6, b"\xff" * 4)), b"", b"\x45", b"\x60" * 39]
+    pkts += [ipv4(1, icmp4(b"\xff" * (stride - 28)))] * 70
+    bad_l4 = bytearray(ipv4(6, tcp_seg(R4, L4, b"ack!")))
+    bad_l4[-1] ^= 4
+    pkts += [bytes(bad_l4)] * 65
+    expect = [O.rx_verify_ref(p, L4, L6, ones_comp=oracle.compute_ones_comp) for p in pkts]
+    st, l4 = run_strided_rx(pkts, stride, 0)
+    got = list(zip(st.tolist(), l4.tolist()))
+    bad = [(i, len(pkts[i]), got[i], expect[i]) for i in range(len(pkts)) if got[i] != tuple(expect[i])]
+    assert not bad, bad[:5]
+
+
+def test_strided_full_size_64B_equals_packed_entry():
+    """bench.py --op verify's c2 batch (2^20 x 64 B IPv4/TCP, every 1009th corrupted) read as
+    64-byte slots: the strided entry's statuses and L4 sums equal the packed entry's, and
+    exactly the planted corruptions are rejected."""
+    from rustnetworkstack_amd.batch import rx_verify_packed, rx_verify_strided
+    from rustnetworkstack_amd.workloads import LOCAL4, LOCAL6, make_verify_batch
+    lay = make_layout("c2_64B")
+    b = DeviceBatch(lay, DEV)
+    make_verify_batch(b)
+    b.launcher(packed=True)
+    assert np.all(lay.off == np.arange(lay.n, dtype=np.uint64) * np.uint64(64))
+    l4a = torch.empty(lay.n, dtype=torch.uint16, device=DEV)
+    l4b = torch.empty(lay.n, dtype=torch.uint16, device=DEV)
+    ref = rx_verify_packed(b.arena, b.blk_off, b.len16, LOCAL4, LOCAL6, l4_sum=l4a).clone()
+    got = rx_verify_strided(b.arena, 64, b.len16, LOCAL4, LOCAL6, l4_sum=l4b)
+    assert torch.equal(got, ref) and torch.equal(l4a, l4b)
+    assert int(((got & _lib.RNS_RX_ACCEPT) == 0).sum().item()) == b.expected_bad
+    del b
+    torch.cuda.empty_cache()

@@ -9,6 +9,9 @@ batch checksum, on the headline batch (2^20 x 1500 B) and on IMIX:
 * verify   — rns_rx_verify_dev: IPv4 header + TCP checks of whole datagrams
 * tx       — rns_tx_fill_dev: IPv4 header + TCP checksums of whole datagrams stored in
              place, pseudo-headers formed on the device
+* tx_packed — rns_tx_fill_packed_dev: the same finalize over the packed form (the rows transmit
+             kernel; round 6)
+* verify_packed — rns_rx_verify_packed_dev: receive verify over the packed form
 * chain_fill — rns_csum_chain_fill_dev on the transmit shape (workloads.tx_chain_layout:
              20-byte TCP head fragments back to back in a header region, the payload as one
              fragment or as 512-byte NetBuffer fragments), next to the plain chain checksum
@@ -31,7 +34,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from rustnetworkstack_amd.batch import (PreparedBatch, csum_chain, csum_fill, csum_fill_packed,  # noqa: E402
-                                        packed_layout, rx_verify, tx_fill)
+                                        packed_layout, rx_verify, rx_verify_packed, tx_fill, tx_fill_packed)
 from rustnetworkstack_amd.workloads import DeviceBatch, make_layout  # noqa: E402
 
 L4 = bytes([192, 168, 1, 2])
@@ -133,6 +136,25 @@ def main():
             filled = int((st == 3).sum().item())
             r["tx"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + n) / ms / 1e6, 1), "filled": filled,
                        "packets": n}
+        if "tx_packed" in ops:
+            write_ipv4_tcp_headers(b, lay, dev)
+            b.launcher(packed=True)  # uploads blk_off / len16
+            st = torch.empty(n, dtype=torch.uint8, device=dev)
+            hint = int(round(lay.mean_len))
+            ms = timed(lambda: tx_fill_packed(b.arena, b.blk_off, b.len16, status=st, len_hint=hint),
+                       args.steps, args.rounds)
+            filled = int((st == 3).sum().item())
+            r["tx_packed"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + n) / ms / 1e6, 1), "filled": filled,
+                              "packets": n}
+        if "verify_packed" in ops:
+            write_ipv4_tcp_headers(b, lay, dev)
+            b.launcher(packed=True)
+            st = torch.empty(n, dtype=torch.uint8, device=dev)
+            ms = timed(lambda: rx_verify_packed(b.arena, b.blk_off, b.len16, L4, L6, status=st),
+                       args.steps, args.rounds)
+            accepted = int((st == 0x43).sum().item())
+            r["verify_packed"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + n) / ms / 1e6, 1),
+                                  "accepted": accepted, "packets": n}
         if "verify" in ops:
             # turn every packet into a valid IPv4/TCP datagram first (header written
             # on the GPU, IPv4 and TCP checksums filled), so every byte is checked
