@@ -577,8 +577,8 @@ class GpuEngine:
         from rustnetworkstack_amd import _lib
         if self.op == "verify":
             if self.verify_strided:
-                return ("csum_strided_rx_kernel (rns_rx_verify_strided_dev: datagrams in fixed-size slots; each lane "
-                        "loads its datagram's first 64 bytes beside its length, two 64-datagram batches per wave)")
+                return ("csum_strided_rx_kernel (rns_rx_verify_strided_dev: datagrams in fixed-size slots; a lane "
+                        "quad per datagram loads its first 64 bytes beside the lengths, one 64-datagram batch per wave)")
             if self.verify_packed:
                 b = self.batches[0]
                 if (b.arena.numel() // max(self.layout.n, 1)) <= 128:

@@ -166,6 +166,9 @@ int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uin
  * fragments are views of whole receive buffers (c3 as [492, 512, 496]: 287 -> 263 us);
  * without such runs the check costs a descriptor round (shuffled 512-byte buffers:
  * 268 -> 283 us), so it is off by default. */
+/* Packets per chain call, at most (both chain entries; the kernel indexes a wave's 64 x 8
+ * packets in 32 bits): a larger n_pkts is RNS_E_INVALID. */
+#define RNS_CHAIN_MAX_PACKETS (0xFFFFFFFFu - 512u)
 int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_frag_off,
                        const uint32_t *d_frag_len, uint32_t n_frags, const uint32_t *d_first,
                        const uint16_t *d_seed, uint16_t *d_out, uint32_t n_pkts, uint32_t flags,
@@ -195,7 +198,8 @@ int rns_csum_chain_dev(const uint8_t *d_arena, uint64_t arena_bytes, const uint6
  * aligned starts (a packed payload region).  Each 64-packet block's payloads then stream
  * as one region (the rows kernel) while every owner sums its own head; a block that does
  * not have this shape takes an exact per-packet loop (slow; use the hint only for such
- * batches). */
+ * batches: a batch whose mean fragment count per packet exceeds 5 ignores the hint and
+ * runs the chain kernel). */
 int rns_csum_chain_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_frag_off,
                             const uint32_t *d_frag_len, uint32_t n_frags, const uint32_t *d_first,
                             const uint16_t *d_seed, const uint16_t *d_field, uint32_t field_off, uint16_t *d_out,
@@ -374,11 +378,25 @@ int rns_csum_batch_multi_dev(const rns_dev_batch *batches, uint32_t nbatches, ui
  * reference's MRU, netif.rs:66); h_off/h_len describe them.  A datagram longer
  * than its slot is dropped (on socket fds recv(MSG_TRUNC) reports its full length),
  * never handed on truncated; max_pkts is capped at INT_MAX.  Returns the number of
- * datagrams (0 on timeout) or RNS_E_IO.  Works on a TUN fd or any datagram fd.
- * rns_io_send_batch writes n datagrams; returns how many were written. */
+ * datagrams (0 on timeout) or RNS_E_IO.  Works on a TUN fd or any datagram fd; on a
+ * socket fd up to 64 datagrams per recvmmsg call.
+ * rns_io_send_batch writes n datagrams (sendmmsg on a socket fd, one writev per datagram
+ * on a TUN fd); returns how many were written. */
 int rns_io_recv_batch(int fd, uint8_t *h_arena, uint64_t slot_bytes, uint32_t max_pkts, uint64_t *h_off,
                       uint32_t *h_len, int timeout_ms);
 int rns_io_send_batch(int fd, const uint8_t *h_arena, const uint64_t *h_off, const uint32_t *h_len, uint32_t n);
+
+/* Batched receive straight into a PACKED arena (the descriptor form of
+ * rns_rx_verify_packed_dev): every queued datagram (after waiting up to timeout_ms for the
+ * first) goes to the next 16-byte boundary of h_arena, as long as a datagram of mru bytes
+ * (<= 65535; the reference's MRU is 2048, netif.rs:66) still fits behind it and fewer than
+ * max_pkts were read.  h_len16[i] = datagram i's length, h_blk_off[b] = the offset of
+ * datagram 64*b, *h_end = the arena bytes used (the last datagram's end rounded up to 16:
+ * what a copy to the GPU needs).  A datagram longer than mru is dropped.  On a socket fd
+ * batches of up to 64 datagrams take one recvmmsg each; a TUN fd takes one read per
+ * datagram.  Returns the number of datagrams (0 on timeout) or RNS_E_IO. */
+int rns_io_recv_batch_packed(int fd, uint8_t *h_arena, uint64_t arena_bytes, uint32_t mru, uint32_t max_pkts,
+                             uint16_t *h_len16, uint64_t *h_blk_off, uint64_t *h_end, int timeout_ms);
 
 /* Pinned host memory for arenas handed to rns_csum_batch_host. */
 int rns_host_alloc(uint64_t bytes, void **out);

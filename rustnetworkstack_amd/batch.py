@@ -57,6 +57,17 @@ def _rx_outputs(dev: torch.device, n: int, status, l4_sum, inputs):
     return status, (l4_sum.data_ptr() if l4_sum is not None else None)
 
 
+def _bad_ptr(bad: torch.Tensor | None, dev: torch.device):
+    """The rejected-descriptor counter the kernels atomically add to: an int32 tensor of at
+    least one entry on the arena's device, or None."""
+    if bad is None:
+        return None
+    _require_cuda(bad, "bad", (torch.int32,))
+    if bad.numel() < 1 or bad.device != dev:
+        raise ValueError(f"bad must be an int32 counter (at least 1 entry) on {dev}")
+    return bad.data_ptr()
+
+
 def _stream_handle(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
@@ -106,10 +117,7 @@ class PreparedBatch:
             _require_cuda(out, "out", _U16)
             if out.numel() != n or out.device != dev:
                 raise ValueError("out must have one entry per packet on the arena's device")
-        bad_ptr = None
-        if bad is not None:
-            _require_cuda(bad, "bad", (torch.int32,))
-            bad_ptr = bad.data_ptr()
+        bad_ptr = _bad_ptr(bad, arena.device)
         lib = _lib.load()
         flags = _lib.RNS_FLAG_COMPLEMENT if complement else 0
         stream = _stream_handle(dev)
@@ -195,10 +203,7 @@ class PackedBatch:
             _require_cuda(out, "out", _U16)
             if out.numel() != n or out.device != dev:
                 raise ValueError("out must have one entry per packet on the arena's device")
-        bad_ptr = None
-        if bad is not None:
-            _require_cuda(bad, "bad", (torch.int32,))
-            bad_ptr = bad.data_ptr()
+        bad_ptr = _bad_ptr(bad, arena.device)
         lib = _lib.load()
         self._keep = (arena, blk_off, len16, seed, out, bad)
         self.out, self.n, self.device = out, n, dev
@@ -272,10 +277,7 @@ class StridedBatch:
             _require_cuda(out, "out", _U16)
             if out.numel() != n or out.device != dev:
                 raise ValueError("out must have one entry per packet on the arena's device")
-        bad_ptr = None
-        if bad is not None:
-            _require_cuda(bad, "bad", (torch.int32,))
-            bad_ptr = bad.data_ptr()
+        bad_ptr = _bad_ptr(bad, arena.device)
         lib = _lib.load()
         self._keep = (arena, seed, out, bad)
         self.out, self.n, self.device = out, int(n), dev
@@ -327,6 +329,8 @@ def csum_chain(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch.Tens
     n = first.numel() - 1
     if frag_len.numel() != nf or n < 0:
         raise ValueError("frag_off/frag_len sizes differ or first is empty")
+    if n > _lib.RNS_CHAIN_MAX_PACKETS or nf >= 2 ** 32:
+        raise ValueError(f"at most {_lib.RNS_CHAIN_MAX_PACKETS} packets and 2^32-1 fragments per chain call")
     dev = arena.device
     seed_ptr = None
     if seed is not None:
@@ -336,7 +340,7 @@ def csum_chain(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch.Tens
         seed_ptr = seed.data_ptr()
     if out is None:
         out = torch.empty(max(n, 0), dtype=torch.uint16, device=dev)
-    bad_ptr = bad.data_ptr() if bad is not None else None
+    bad_ptr = _bad_ptr(bad, arena.device)
     lib = _lib.load()
     with torch.cuda.device(dev):
         st = lib.rns_csum_chain_dev(arena.data_ptr(), arena.numel(), frag_off.data_ptr(), frag_len.data_ptr(), nf,
@@ -370,8 +374,8 @@ def csum_chain_fill(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch
     n = first.numel() - 1
     if frag_len.numel() != nf or n < 0:
         raise ValueError("frag_off/frag_len sizes differ or first is empty")
-    if n >= 2 ** 32 or nf >= 2 ** 32:
-        raise ValueError("at most 2^32-1 packets and fragments per call")
+    if n > _lib.RNS_CHAIN_MAX_PACKETS or nf >= 2 ** 32:
+        raise ValueError(f"at most {_lib.RNS_CHAIN_MAX_PACKETS} packets and 2^32-1 fragments per chain call")
     dev = arena.device
     for name, t in (("frag_off", frag_off), ("frag_len", frag_len), ("first", first)):
         if t.device != dev:
@@ -387,10 +391,7 @@ def csum_chain_fill(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch
         ptrs.append(t.data_ptr())
     if field is None and not 0 <= int(field_off) < 2 ** 32:
         raise ValueError("field_off must be a u32")
-    bad_ptr = None
-    if bad is not None:
-        _require_cuda(bad, "bad", (torch.int32,))
-        bad_ptr = bad.data_ptr()
+    bad_ptr = _bad_ptr(bad, arena.device)
     flags = (_lib.RNS_FLAG_COMPLEMENT if complement else 0) | (_lib.RNS_FLAG_CHAIN_RUNS if runs else 0) | \
         (_lib.RNS_FLAG_CHAIN_TX_PACKED if tx_packed else 0)
     with torch.cuda.device(dev):
@@ -427,10 +428,7 @@ def csum_fill(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, seed
         if t.numel() != n or t.device != dev:
             raise ValueError(f"{name} must have one entry per packet on the arena's device")
         ptrs.append(t.data_ptr())
-    bad_ptr = None
-    if bad is not None:
-        _require_cuda(bad, "bad", (torch.int32,))
-        bad_ptr = bad.data_ptr()
+    bad_ptr = _bad_ptr(bad, arena.device)
     lib = _lib.load()
     with torch.cuda.device(dev):
         st = lib.rns_csum_fill_dev(arena.data_ptr(), arena.numel(), off.data_ptr(), length.data_ptr(), ptrs[0],
@@ -471,12 +469,7 @@ def csum_fill_packed(arena: torch.Tensor, blk_off: torch.Tensor, len16: torch.Te
         if t.numel() != n or t.device != dev:
             raise ValueError(f"{name} must have one entry per packet on the arena's device")
         ptrs.append(t.data_ptr())
-    bad_ptr = None
-    if bad is not None:
-        _require_cuda(bad, "bad", (torch.int32,))
-        if bad.device != dev:
-            raise ValueError(f"bad is on {bad.device}, arena on {dev}")
-        bad_ptr = bad.data_ptr()
+    bad_ptr = _bad_ptr(bad, arena.device)
     lib = _lib.load()
     with torch.cuda.device(dev):
         st = lib.rns_csum_fill_packed_dev(arena.data_ptr(), arena.numel(), blk_off.data_ptr(), len16.data_ptr(),
@@ -648,6 +641,31 @@ def recv_batch(fd: int, arena: np.ndarray, slot_bytes: int = 2048, max_pkts: int
     if r < 0:
         raise _lib.ChecksumError(r, "rns_io_recv_batch")
     return off[:r], ln[:r]
+
+
+def recv_batch_packed(fd: int, arena: np.ndarray, mru: int = 2048, max_pkts: int | None = None,
+                      timeout_ms: int = 0) -> tuple[np.ndarray, np.ndarray, int]:
+    """Read every queued datagram (after waiting up to ``timeout_ms`` for the first) into
+    ``arena`` PACKED: each at the next 16-byte boundary while a datagram of ``mru`` bytes
+    still fits (rns_io_recv_batch_packed).  Returns (lengths uint16 [n], blk_off uint64
+    [ceil(n/64)], end) — the packed form's descriptors (rx_verify_packed) and the bytes used."""
+    if arena.dtype != np.uint8 or not arena.flags["C_CONTIGUOUS"]:
+        raise ValueError("arena must be a contiguous uint8 array")
+    if not 0 < int(mru) <= 0xFFFF:
+        raise ValueError("mru must be in 1..65535 (the packed form's lengths are u16)")
+    cap = arena.shape[0] // 16  # no more datagrams than 16-byte slots
+    max_pkts = cap if max_pkts is None else min(int(max_pkts), cap)
+    max_pkts = min(max_pkts, 2 ** 31 - 1)
+    ln = np.empty(max(max_pkts, 1), dtype=np.uint16)
+    blk = np.empty(max((max_pkts + 63) // 64, 1), dtype=np.uint64)
+    end = ctypes.c_uint64(0)
+    if max_pkts <= 0:
+        return ln[:0], blk[:0], 0
+    r = _lib.load().rns_io_recv_batch_packed(int(fd), arena.ctypes.data, arena.shape[0], int(mru), max_pkts,
+                                             ln.ctypes.data, blk.ctypes.data, ctypes.byref(end), int(timeout_ms))
+    if r < 0:
+        raise _lib.ChecksumError(r, "rns_io_recv_batch_packed")
+    return ln[:r], blk[:(r + 63) // 64], int(end.value)
 
 
 def send_batch(fd: int, arena: np.ndarray, off: np.ndarray, length: np.ndarray) -> int:

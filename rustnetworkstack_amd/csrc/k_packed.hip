@@ -98,6 +98,9 @@ int dispatch_packed(const CsumArgs &a, const Shape &sh, hipStream_t st)
 
 // Transmit fill of a packed arena (align_log2 >= 4): the rows kernel in fill mode, D by the
 // typical length as for the plain checksum.
+// (Temporal row loads, so that a field's line is still in L2 when its store comes, measured
+// slower on c3 and equal on IMIX: fill 344.4 / 762.3 us, finalize 360.8 / 808.8 against
+// 303.8 / 764.2 and 306.7 / 810.9 with nontemporal rows; session r06d.)
 int launch_fill_packed(const CsumArgs &a, hipStream_t st)
 {
     constexpr bool NT = RNS_STREAM_NT != 0;
@@ -141,10 +144,12 @@ int launch_tx_packed(const CsumArgs &a, hipStream_t st)
     return hip_status(hipGetLastError());
 }
 
-// Receive verify of datagrams at a fixed stride: B batches of 64 per one-wave workgroup.
+// Receive verify of datagrams at a fixed stride: B batches of 64 per one-wave workgroup (one:
+// 48 VGPRs, 10 waves/SIMD; two batches per wave need 81 VGPRs and a second generation of waves,
+// 16.4 us per isolated 64-byte dispatch against 14.0: sessions r06c, r06d).
 int launch_strided_rx(const CsumArgs &a, hipStream_t st)
 {
-    constexpr int B = RNS_STRIDED_RX_B;
+    constexpr int B = kStridedRxB;
     const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 64 * B - 1) / (64 * B))), block(64);
     if (buf_records(a) < kOobOffset)
         hipLaunchKernelGGL((csum_strided_rx_kernel<true, B>), grid, block, 0, st, a);

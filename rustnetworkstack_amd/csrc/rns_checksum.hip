@@ -220,7 +220,8 @@ static int chain_launch(CsumArgs &a, const uint64_t *d_frag_off, const uint32_t 
 {
     // the chain kernel adds packet indices in 32 bits (a VGPR less across its class pass): its
     // last wave's base + 64 * K + lane must not wrap
-    if (n_pkts > 0xFFFFFFFFu - 64u * kChainMaxK)
+    static_assert(RNS_CHAIN_MAX_PACKETS == 0xFFFFFFFFu - 64u * kChainMaxK, "rns_checksum.h's chain cap");
+    if (n_pkts > RNS_CHAIN_MAX_PACKETS)
         return RNS_E_INVALID;
     a.off = d_frag_off;
     a.len = d_frag_len;
@@ -242,7 +243,11 @@ static int chain_launch(CsumArgs &a, const uint64_t *d_frag_off, const uint32_t 
         }
     }
     a.chain_k = K;
-    if (flags & RNS_FLAG_CHAIN_TX_PACKED)  // transmit-shaped chains: heads + a packed payload region
+    // transmit-shaped chains: heads + a packed payload region.  A batch whose mean fragment
+    // count already exceeds the shape (a head + kRunFrags payload fragments) has most of its
+    // waves in the transmit-rows kernel's exact per-packet loop — far slower than the chain
+    // kernel on the same chains — so the hint is ignored there (same results either way).
+    if ((flags & RNS_FLAG_CHAIN_TX_PACKED) && mean <= 1.0 + kRunFrags)
         return launch_txrows<FILL>(a, stream);
     // Nontemporal loads for NetBuffer-sized fragments (c3 as 3 fragments: 298 -> 289 us
     // packed back to back, 281 -> 261 us in 512-byte buffers), not for IMIX's mix of
@@ -306,9 +311,7 @@ int rns_csum_chain_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64
 // wave looping over several batches: one-batch waves are mostly launch ramp there (64 B
 // verify 18.9 -> 17.2-17.8 us per step); larger datagrams keep one wave per batch (a cap
 // measured 3-6 % slower on IMIX; profiles/r02_rx_cap_ab.json).
-#ifndef RNS_RX_GRID_CAP  // A/B knob: the cap for tiny datagrams; 0 = none
-#define RNS_RX_GRID_CAP 4096
-#endif
+constexpr uint64_t kRxGridCap = 4096;  // the cap for tiny datagrams
 // Receive verify and transmit finalize take the cap (64 B finalize 35.2-36.3 -> 33.3 us);
 // the single-field fill does not (64 B fill 28.9-29.2 us without, 29.8-30.0 with it:
 // profiles/r02_tx_cap_ab.json).
@@ -316,9 +319,9 @@ static uint64_t stash_blocks(uint64_t n, uint64_t arena_bytes, bool tiny_cap)
 {
     constexpr int BLK = kMixedBlock<true>;
     uint64_t blocks = ((n + 63) / 64 + BLK / 64 - 1) / (BLK / 64);
-    const bool cap = RNS_RX_GRID_CAP != 0 && tiny_cap && arena_bytes / n <= 128;
-    if (cap && blocks > RNS_RX_GRID_CAP)
-        blocks = RNS_RX_GRID_CAP;
+    const bool cap = tiny_cap && arena_bytes / n <= 128;
+    if (cap && blocks > kRxGridCap)
+        blocks = kRxGridCap;
     return blocks;
 }
 

@@ -431,82 +431,137 @@ __global__ __launch_bounds__(64, RNS_ROWS_RX_OCC) void csum_rows_rx_kernel(const
 // Receive verify of datagrams at a fixed stride (rns_rx_verify_strided_dev, round 6):
 // datagram i = arena[first_off + i * stride, + len16[i]) — a receive ring of fixed-size slots
 // (64-byte ACK slots, or the reference's 2048-byte MRU buffers, netif.rs:66).  No block offsets
-// and no scan: every lane computes its datagram's address itself, so with 16-byte-aligned
-// slots its first 4 chunks (64 bytes) are loaded together with its length — one memory latency
-// for the descriptors and the bytes of an ACK-sized datagram, where the packed form's ACK path
-// waits for the block offset, scans the lengths, and only then loads (the prologue the strided
-// tiny kernel took off the 64-byte checksum).  A datagram longer than 64 bytes is summed by
-// the whole wave, one datagram at a time (as the packed kernels' unaligned path); its header
-// is in the same 4 chunks.  Unaligned slots take that loop for every datagram and load their
-// header chunks from the 16-byte boundary below the start.  B 64-datagram batches per wave.
+// and no scan: the lanes compute every address themselves.  With 16-byte-aligned slots a
+// 64-datagram batch is read as csum_strided_tiny_kernel reads c2 — 4 rows, lane 4k + j loading
+// chunk j of datagram 16r + k in row r (one coalesced KiB per row for 64-byte slots) — and
+// lane 4k + j OWNS datagram 16j + k, so everything a datagram's finish needs stays in its quad:
+// per row the quad sums its datagram's first 64 bytes (T) and its header bytes (H, IHL from
+// byte 0 broadcast in the quad), and the owner (quad lane r) takes T, H and the first 24 bytes
+// with quad DPP moves — no LDS, no ds_bpermute.  (Lane-per-datagram loads, as the packed
+// form's ACK path does, measured 15.1-15.6 us per isolated dispatch on 1M x 64 B: r06b.)  A
+// datagram longer than 64 bytes has its whole sum taken by the wave, one datagram at a time
+// (as the packed kernels' unaligned path); its header is in the quad's 64 bytes.  Unaligned
+// slots take that loop for every datagram and load their header chunks from the 16-byte
+// boundary below the start.  B 64-datagram batches per wave.
 // ---------------------------------------------------------------------------
-#ifndef RNS_STRIDED_RX_B  // 64-datagram batches per wave of the strided receive kernel
-#define RNS_STRIDED_RX_B 2
-#endif
-#ifndef RNS_STRIDED_RX_AUX  // cache-policy bits of its slot loads (A/B)
-#define RNS_STRIDED_RX_AUX 0
-#endif
+constexpr int kStridedRxB = 1;    // 64-datagram batches per wave (k_packed.hip: launch_strided_rx)
+constexpr int kStridedRxOcc = 8;  // waves/SIMD bound (48 VGPRs: 10 fit)
 template <bool BUF, int B>
-__global__ __launch_bounds__(64) void csum_strided_rx_kernel(const CsumArgs a)
+__global__ __launch_bounds__(64, kStridedRxOcc) void csum_strided_rx_kernel(const CsumArgs a)
 {
     const uint32_t lane = threadIdx.x;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
     const uint64_t recs = buf_records(a);
     const uint64_t start0 = a.first_off + a.base_adjust;
-    const bool aligned = ((start0 | a.stride) & 15) == 0;  // uniform: a kernel argument
+    const bool aligned = ((start0 | a.stride) & 15) == 0;  // uniform: kernel arguments
+    const uint32_t k = lane >> 2, j = lane & 3;
+    const uint32_t dl = 16u * j + k;  // the datagram this lane owns, in its batch
     uint32_t len[B];
-    uint64_t st[B];
-    uint4 own[B][4];
+    uint4 x[B][4];  // row r: chunk j of datagram 16r + k
 #pragma unroll
     for (int b = 0; b < B; ++b) {
-        const uint64_t p = (static_cast<uint64_t>(blockIdx.x) * B + b) * 64 + lane;
-        const bool live = p < a.n;
-        len[b] = live ? static_cast<uint32_t>(a.len16[live ? p : a.n - 1]) : 0u;
-        st[b] = start0 + p * a.stride;
-        // chunks 0-3 of the slot, issued beside the length (zero past the arena; bytes past the
-        // datagram are masked once its length is known)
+        const uint64_t base = (static_cast<uint64_t>(blockIdx.x) * B + b) * 64;
+        const uint64_t p = base + dl;
+        len[b] = p < a.n ? static_cast<uint32_t>(a.len16[p]) : 0u;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint64_t o = st[b] + 16u * i;
-            const bool in = aligned && live && o + 16 <= recs && st[b] <= a.arena_bytes;
+        for (int r = 0; r < 4; ++r) {
+            const uint64_t q = base + 16u * r + k;
+            const uint64_t o = start0 + q * a.stride + 16u * j;
+            const bool in = aligned && q < a.n && o + 16 <= recs;
             if constexpr (BUF) {
-                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, in ? static_cast<uint32_t>(o) : kOobOffset,
-                                                                      0, RNS_STRIDED_RX_AUX);
-                own[b][i] = make_uint4(x.x, x.y, x.z, x.w);
+                const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rsrc, in ? static_cast<uint32_t>(o) : kOobOffset,
+                                                                      0, kNtAux);
+                x[b][r] = make_uint4(y.x, y.y, y.z, y.w);
             } else {
-                const uint4 x = load_chunk<false>(a.arena + (in ? o : 0));
-                own[b][i] = in ? x : make_uint4(0, 0, 0, 0);
+                const uint4 y = load_chunk<true>(a.arena + (in ? o : 0));
+                x[b][r] = in ? y : make_uint4(0, 0, 0, 0);
             }
         }
     }
 #pragma unroll
     for (int b = 0; b < B; ++b) {
-        const uint64_t p = (static_cast<uint64_t>(blockIdx.x) * B + b) * 64 + lane;
+        const uint64_t p = (static_cast<uint64_t>(blockIdx.x) * B + b) * 64 + dl;
         const bool live = p < a.n;
         const uint32_t L = len[b];
-        const uint64_t start = st[b];
+        const uint64_t start = start0 + p * a.stride;
         const bool ok = start <= a.arena_bytes && L <= a.arena_bytes - start;
         const bool present = live && ok && L != 0;
         uint32_t mine = 0;
-        uint4 hd[5];
-        hd[4] = make_uint4(0, 0, 0, 0);
+        uint8_t stv;
+        uint32_t l4_res = 0;
         if (aligned) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                uint4 x = own[b][i];
-                if (16u * i + 16u > L)  // an ACK-sized datagram's bytes past its end never count
-                    x = 16u * i < L ? keep_first(x, L - 16u * i) : make_uint4(0, 0, 0, 0);
-                hd[i] = x;
-                mine = __builtin_amdgcn_sad_u16(x.x, 0, mine);
-                mine = __builtin_amdgcn_sad_u16(x.y, 0, mine);
-                mine = __builtin_amdgcn_sad_u16(x.z, 0, mine);
-                mine = __builtin_amdgcn_sad_u16(x.w, 0, mine);
+            uint32_t H = 0, head[6] = {0, 0, 0, 0, 0, 0};
+            auto row = [&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                const uint32_t Lr = dpp_mov<r * 0x55>(L);  // the row's datagram 16r + k: owned by quad lane r
+                uint4 xm = x[b][r];
+                if (16u * j + 16u > Lr)  // bytes past the datagram never count
+                    xm = 16u * j < Lr ? keep_first(xm, Lr - 16u * j) : make_uint4(0, 0, 0, 0);
+                uint32_t t = __builtin_amdgcn_sad_u16(xm.x, 0, 0u);
+                t = __builtin_amdgcn_sad_u16(xm.y, 0, t);
+                t = __builtin_amdgcn_sad_u16(xm.z, 0, t);
+                t = __builtin_amdgcn_sad_u16(xm.w, 0, t);
+                t = group_allreduce<4>(t);
+                const uint32_t c0x = dpp_mov<0x00>(xm.x), c0y = dpp_mov<0x00>(xm.y);  // chunk 0 (quad lane 0)
+                const uint32_t c0z = dpp_mov<0x00>(xm.z), c0w = dpp_mov<0x00>(xm.w);
+                const uint32_t c1x = dpp_mov<0x55>(xm.x), c1y = dpp_mov<0x55>(xm.y);  // chunk 1 (quad lane 1)
+                const uint32_t b0 = c0x & 0xffu, v = b0 >> 4;
+                const uint32_t hdr = v == 4 ? (b0 & 15u) * 4u : v == 6 ? 40u : 0u;  // <= 60
+                uint4 hm = make_uint4(0, 0, 0, 0);
+                if (16u * j < hdr)
+                    hm = 16u * j + 16u <= hdr ? xm : keep_first(xm, hdr - 16u * j);
+                uint32_t h = __builtin_amdgcn_sad_u16(hm.x, 0, 0u);
+                h = __builtin_amdgcn_sad_u16(hm.y, 0, h);
+                h = __builtin_amdgcn_sad_u16(hm.z, 0, h);
+                h = __builtin_amdgcn_sad_u16(hm.w, 0, h);
+                h = group_allreduce<4>(h);
+                if (j == static_cast<uint32_t>(r)) {
+                    mine = t;
+                    H = h;
+                    head[0] = c0x;
+                    head[1] = c0y;
+                    head[2] = c0z;
+                    head[3] = c0w;
+                    head[4] = c1x;
+                    head[5] = c1y;
+                }
+            };
+            row(std::integral_constant<int, 0>{});
+            row(std::integral_constant<int, 1>{});
+            row(std::integral_constant<int, 2>{});
+            row(std::integral_constant<int, 3>{});
+            uint64_t todo = __ballot(present && L > 64);
+            while (todo) {  // longer datagrams: the whole wave sums one at a time
+                const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
+                todo &= todo - 1;
+                const uint64_t sto =
+                    (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start >> 32), o)))
+                     << 32) |
+                    static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start), o));
+                const Pkt pk = make_pkt(sto, __builtin_amdgcn_readlane(L, o));
+                uint32_t acc = 0;
+                for (uint32_t cc = 0; cc < pk.nch; cc += 64) {
+                    uint4 w[1];
+                    issue_pass<64, 1, true, BUF, 1>(a, rsrc, pk, cc + lane, w);
+                    mask_edges<64, 1, 1>(pk, cc + lane, w);
+                    acc = sum_le<1, 1>(w, acc);
+                }
+                const uint32_t sum = group_allreduce<64>(acc);
+                mine = lane == o ? sum : mine;
             }
-        }
-        uint64_t todo = __ballot(present && (!aligned || L > 64));
-        if (todo) {
-            // ---- longer (or unaligned) datagrams: the whole wave sums one at a time ----
+            // rx_finish with H and the header dwords from the quad (16-byte-aligned: even starts)
+            const RxParse rp = present ? rx_parse(head, L, a.local4_sum, a.local6_sum) : RxParse{kMetaMalformed, 0u, 0u};
+            uint32_t hdr_res = 0;
+            if (!(rp.meta & kMetaMalformed)) {
+                hdr_res = finalize_bits(H, false, false, 0u, true, RNS_FLAG_COMPLEMENT);
+                if (rp.meta & kMetaL4Checked)
+                    l4_res = finalize_bits(mine - H, false, false, rp.ph, true, RNS_FLAG_COMPLEMENT);
+            }
+            stv = rx_verdict(rp.meta, hdr_res, l4_res);
+        } else {
+            // ---- unaligned slots (rare): the whole wave sums one datagram at a time ----
+            uint64_t todo = __ballot(present);
             while (todo) {
                 const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
                 todo &= todo - 1;
@@ -514,28 +569,22 @@ __global__ __launch_bounds__(64) void csum_strided_rx_kernel(const CsumArgs a)
                     (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start >> 32), o)))
                      << 32) |
                     static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(start), o));
-                const uint32_t Lo = __builtin_amdgcn_readlane(L, o);
-                const Pkt k = make_pkt(sto, Lo);
+                const Pkt pk = make_pkt(sto, __builtin_amdgcn_readlane(L, o));
                 uint32_t acc = 0;
-                for (uint32_t cc = 0; cc < k.nch; cc += 64) {
+                for (uint32_t cc = 0; cc < pk.nch; cc += 64) {
                     uint4 w[1];
-                    issue_pass<64, 1, true, BUF, 1>(a, rsrc, k, cc + lane, w);
-                    mask_edges<64, 1, 1>(k, cc + lane, w);
+                    issue_pass<64, 1, true, BUF, 1>(a, rsrc, pk, cc + lane, w);
+                    mask_edges<64, 1, 1>(pk, cc + lane, w);
                     acc = sum_le<1, 1>(w, acc);
                 }
                 const uint32_t sum = group_allreduce<64>(acc);
                 mine = lane == o ? sum : mine;
             }
-        }
-        uint8_t stv;
-        uint32_t l4_res = 0;
-        if (aligned) {
-            stv = rx_finish<4>(a, hd, mine, 0u, L, false, false, present, l4_res);
-        } else {
             // the header from the 16-byte boundary below the start: 5 chunks hold its first
             // 65-80 bytes, masked to the datagram
             const uint64_t b0 = start & ~15ull;
             const uint32_t s0 = static_cast<uint32_t>(start & 15);
+            uint4 hd[5];
 #pragma unroll
             for (int i = 0; i < 5; ++i) {
                 hd[i] = own_chunk<BUF>(a, rsrc, recs, b0, present ? s0 + L : 0u, i);
@@ -545,7 +594,7 @@ __global__ __launch_bounds__(64) void csum_strided_rx_kernel(const CsumArgs a)
             }
             stv = rx_finish<5>(a, hd, mine, s0, L, start & 1, false, present, l4_res);
         }
-        if (live) {
+        if (live) {  // lane 4k + j: datagram 16j + k (a permutation of 64 consecutive entries)
             a.status[p] = stv;
             if (a.l4_out)
                 a.l4_out[p] = static_cast<uint16_t>(l4_res);

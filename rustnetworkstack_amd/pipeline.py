@@ -1,7 +1,10 @@
 """End-to-end batched receive and transmit.
 
 Receive (RxPipeline): datagram fd -> pinned host arena -> HBM -> fused receive verify
--> per-packet verdicts.  Transmit (TxPipeline): pinned slots -> HBM -> transmit
+-> per-packet verdicts.  By default the datagrams are received PACKED (each at the next
+16-byte boundary, rns_io_recv_batch_packed), so the copy to the GPU carries their bytes
+only — not whole 2048-byte slots — and the verify is the rows receive kernel
+(rns_rx_verify_packed_dev); ``packed=False`` keeps MRU slots and rns_rx_verify_dev.  Transmit (TxPipeline): pinned slots -> HBM -> transmit
 finalize -> the changed header bytes back -> datagram fd.
 
 The reference handles one packet per loop iteration on its receive thread
@@ -23,15 +26,16 @@ from typing import Iterator
 import numpy as np
 import torch
 
-from .batch import PinnedBuffer, recv_batch, rx_verify, send_batch, tx_fill
+from .batch import PinnedBuffer, recv_batch, recv_batch_packed, rx_verify, rx_verify_packed, send_batch, tx_fill
 
 MRU = 2048  # netif.rs:66
 
 
 class _Slots:
-    """One buffer set: pinned host slots + lengths + per-slot results, and their HBM twins."""
+    """One buffer set: pinned host slots + lengths + per-slot results, and their HBM twins
+    (packed: u16 lengths and one block offset per 64 datagrams instead of u32 lengths)."""
 
-    def __init__(self, dev: torch.device, max_pkts: int, slot_bytes: int, head: int = 0):
+    def __init__(self, dev: torch.device, max_pkts: int, slot_bytes: int, head: int = 0, packed: bool = False):
         self.host = PinnedBuffer(slot_bytes * max_pkts)
         self.h_len = PinnedBuffer(4 * max_pkts)
         self.h_status = PinnedBuffer(max_pkts)
@@ -39,87 +43,138 @@ class _Slots:
         self.d_arena = torch.empty(slot_bytes * max_pkts, dtype=torch.uint8, device=dev)
         self.d_len = torch.empty(max_pkts, dtype=torch.int32, device=dev)
         self.d_status = torch.empty(max_pkts, dtype=torch.uint8, device=dev)
+        nblk = (max_pkts + 63) // 64
+        self.h_blk = PinnedBuffer(8 * nblk) if packed else None
+        self.d_blk = torch.empty(nblk, dtype=torch.int64, device=dev) if packed else None
         self.done = torch.cuda.Event()
 
     def close(self):
-        for b in (self.host, self.h_len, self.h_status, self.h_head):
+        for b in (self.host, self.h_len, self.h_status, self.h_head, self.h_blk):
             if b is not None:
                 b.free()
 
 
+class Datagrams:
+    """The datagrams of one received batch: ``d[i]`` is datagram i's bytes (a view of the
+    pinned arena, valid until the buffer set is reused)."""
+
+    def __init__(self, arena: np.ndarray, off: np.ndarray, length: np.ndarray):
+        self.arena, self.off, self.length = arena, off, length
+
+    def __len__(self) -> int:
+        return int(self.length.shape[0])
+
+    def __getitem__(self, i: int) -> np.ndarray:
+        o = int(self.off[i])
+        return self.arena[o:o + int(self.length[i])]
+
+
 class RxPipeline:
     def __init__(self, local_ipv4: bytes, local_ipv6: bytes, device: int = 0, max_pkts: int = 65536,
-                 slot_bytes: int = MRU):
+                 slot_bytes: int = MRU, packed: bool = True):
         self.local_ipv4, self.local_ipv6 = bytes(local_ipv4), bytes(local_ipv6)
-        self.slot = slot_bytes
+        self.slot = slot_bytes  # the MRU: the arena holds max_pkts datagrams of this size
         self.max_pkts = max_pkts
+        self.packed = packed
         self.dev = torch.device(f"cuda:{device}")
-        self._sets = [_Slots(self.dev, max_pkts, slot_bytes)]
+        self._sets = [_Slots(self.dev, max_pkts, slot_bytes, packed=packed)]
         self.d_off = (torch.arange(max_pkts, dtype=torch.int64, device=self.dev) * slot_bytes).contiguous()
         self._stream = None
+        self.h2d_bytes = 0  # arena bytes copied to the GPU so far (packed: the datagrams' 16-byte-padded bytes)
+        self.datagrams = 0
+        self.last: Datagrams | None = None  # the datagrams of the last batch ``receive`` returned
 
     @property
     def host(self) -> PinnedBuffer:
-        """Set 0's pinned slots: where ``receive`` leaves packet i (slot i)."""
+        """Set 0's pinned arena: where ``receive`` leaves its datagrams (``last``)."""
         return self._sets[0].host
 
-    def _submit(self, s: _Slots, ln: np.ndarray) -> None:
-        """Queue H2D + verify + status D2H of the first len(ln) slots of ``s`` on the
-        current stream; ``s.done`` marks the status landing in pinned memory."""
+    def _read(self, s: _Slots, fd: int, timeout_ms: int):
+        """One batched read into set ``s``: (lengths, Datagrams, arena bytes used)."""
+        if self.packed:
+            ln16, blk, end = recv_batch_packed(fd, s.host.array, self.slot, self.max_pkts, timeout_ms)
+            n = ln16.shape[0]
+            if n:
+                s.h_blk.array.view(np.uint64)[: blk.shape[0]] = blk
+            pad = (ln16.astype(np.uint64) + np.uint64(15)) & ~np.uint64(15)
+            off = np.zeros(n, dtype=np.uint64)
+            if n > 1:
+                np.cumsum(pad[:-1], out=off[1:])
+            return ln16.astype(np.uint32), Datagrams(s.host.array, off, ln16), end
+        off, ln = recv_batch(fd, s.host.array, self.slot, self.max_pkts, timeout_ms)
+        return ln, Datagrams(s.host.array, off, ln), ln.shape[0] * self.slot
+
+    def _submit(self, s: _Slots, ln: np.ndarray, used: int) -> None:
+        """Queue H2D + verify + status D2H of the batch in ``s`` (len(ln) datagrams in its
+        first ``used`` arena bytes) on the current stream; ``s.done`` marks the status
+        landing in pinned memory."""
         n = ln.shape[0]
-        hl = s.h_len.array.view(np.uint32)[:n]
-        hl[:] = ln
         # pinned host memory (rns_host_alloc): every copy is a DMA transfer
-        s.d_arena[: n * self.slot].copy_(torch.from_numpy(s.host.array[: n * self.slot]), non_blocking=True)
-        s.d_len[:n].copy_(torch.from_numpy(hl.view(np.int32)), non_blocking=True)
-        rx_verify(s.d_arena, self.d_off[:n], s.d_len[:n], self.local_ipv4, self.local_ipv6, status=s.d_status[:n])
+        s.d_arena[:used].copy_(torch.from_numpy(s.host.array[:used]), non_blocking=True)
+        self.h2d_bytes += used
+        self.datagrams += n
+        if self.packed:
+            h16 = s.h_len.array.view(np.uint16)[:n]
+            h16[:] = ln
+            nb = (n + 63) // 64
+            d16 = s.d_len.view(torch.int16)[:n]
+            d16.copy_(torch.from_numpy(h16.view(np.int16)), non_blocking=True)
+            s.d_blk[:nb].copy_(torch.from_numpy(s.h_blk.array.view(np.int64)[:nb]), non_blocking=True)
+            rx_verify_packed(s.d_arena[:max(used, 1)], s.d_blk[:nb], d16, self.local_ipv4, self.local_ipv6,
+                             status=s.d_status[:n])
+        else:
+            hl = s.h_len.array.view(np.uint32)[:n]
+            hl[:] = ln
+            s.d_len[:n].copy_(torch.from_numpy(hl.view(np.int32)), non_blocking=True)
+            rx_verify(s.d_arena, self.d_off[:n], s.d_len[:n], self.local_ipv4, self.local_ipv6,
+                      status=s.d_status[:n])
         torch.from_numpy(s.h_status.array[:n]).copy_(s.d_status[:n], non_blocking=True)
         s.done.record()
 
     def receive(self, fd: int, timeout_ms: int = 0) -> tuple[np.ndarray, np.ndarray]:
-        """One batch: returns (status uint8 [n], lengths uint32 [n]); packet i is in
-        slot i of ``self.host.array``."""
+        """One batch: returns (status uint8 [n], lengths uint32 [n]); ``self.last[i]`` is
+        datagram i's bytes in the pinned arena."""
         s = self._sets[0]
-        off, ln = recv_batch(fd, s.host.array, self.slot, self.max_pkts, timeout_ms)
-        n = off.shape[0]
+        ln, dg, used = self._read(s, fd, timeout_ms)
+        self.last = dg
+        n = ln.shape[0]
         if n == 0:
             return np.empty(0, dtype=np.uint8), ln
         with torch.cuda.device(self.dev):
-            self._submit(s, ln)
+            self._submit(s, ln, used)
             s.done.synchronize()
         return s.h_status.array[:n].copy(), ln
 
-    def stream(self, fd: int, timeout_ms: int = 0) -> Iterator[tuple[np.ndarray, np.ndarray, np.ndarray]]:
-        """Overlapped receive: yields (status [n], lengths [n], slots [n, slot_bytes])
-        per batch until a read finds nothing within ``timeout_ms``.  While batch k is
-        on the GPU the host reads batch k+1 into the other buffer set; the yielded
-        arrays stay valid until the generator is resumed."""
+    def stream(self, fd: int, timeout_ms: int = 0) -> Iterator[tuple[np.ndarray, np.ndarray, Datagrams]]:
+        """Overlapped receive: yields (status [n], lengths [n], Datagrams) per batch until a
+        read finds nothing within ``timeout_ms``.  While batch k is on the GPU the host reads
+        batch k+1 into the other buffer set; the yielded arrays stay valid until the
+        generator is resumed."""
         if len(self._sets) == 1:
-            self._sets.append(_Slots(self.dev, self.max_pkts, self.slot))
+            self._sets.append(_Slots(self.dev, self.max_pkts, self.slot, packed=self.packed))
         if self._stream is None:
             self._stream = torch.cuda.Stream(self.dev)
-        pending = None  # (set, lengths) on the GPU
+        pending = None  # (set, lengths, datagrams) on the GPU
         k = 0
         while True:
             s = self._sets[k]
             if pending is None:
-                off, ln = recv_batch(fd, s.host.array, self.slot, self.max_pkts, timeout_ms)
+                ln, dg, used = self._read(s, fd, timeout_ms)
             else:
                 # take what is queued now (no wait), hand the finished batch over, and
                 # only then block for more: the last batch is not held back by the timeout
-                off, ln = recv_batch(fd, s.host.array, self.slot, self.max_pkts, 0)
-                p, pln = pending
+                ln, dg, used = self._read(s, fd, 0)
+                p, pln, pdg = pending
                 p.done.synchronize()
-                n = pln.shape[0]
-                yield p.h_status.array[:n], pln, p.host.array[: n * self.slot].reshape(n, self.slot)
+                yield p.h_status.array[: pln.shape[0]], pln, pdg
                 pending = None
-                if off.shape[0] == 0:
-                    off, ln = recv_batch(fd, s.host.array, self.slot, self.max_pkts, timeout_ms)
-            if off.shape[0] == 0:
+                if ln.shape[0] == 0:
+                    ln, dg, used = self._read(s, fd, timeout_ms)
+            if ln.shape[0] == 0:
                 return
             with torch.cuda.device(self.dev), torch.cuda.stream(self._stream):
-                self._submit(s, ln)
-            pending = (s, ln)
+                self._submit(s, ln, used)
+            pending = (s, ln, dg)
             k ^= 1
 
     def close(self):

@@ -537,6 +537,101 @@ static int test_tx_rx(hipStream_t st)
     return 0;
 }
 
+/* The packed transmit arena (rns_tx_fill_packed_dev: the rows transmit kernel) and its packed
+ * receive (rns_rx_verify_packed_dev), then the same datagrams in 2048-byte receive slots
+ * (rns_rx_verify_strided_dev): IPv4 TCP / UDP / ICMP with garbage in the checksum fields;
+ * every field must hold what the transmit call sites store (the oracle's util.rs functions
+ * over the datagram with the field zeroed), every other byte — the padding between datagrams
+ * included — unchanged, and the receiver accepts them all. */
+static int test_tx_rx_packed(hipStream_t st)
+{
+    const uint32_t n = 2500;
+    const uint8_t src[4] = {10, 0, 0, 1}, dst[4] = {10, 0, 0, 2}, dst6[16] = {0xfd, [15] = 2};
+    uint16_t *len16 = malloc(n * sizeof *len16);
+    uint64_t *off = malloc(n * sizeof *off), *blk = malloc(((n + 63) / 64) * sizeof *blk), end = 0;
+    uint8_t *proto = malloc(n), *status = malloc(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t r = next_u64();
+        len16[i] = (uint16_t)(40u + (uint32_t)((r >> 8) % 1461u));
+        proto[i] = (i % 3 == 0) ? 6 : (i % 3 == 1) ? 17 : 1;
+    }
+    CHECK(rns_packed_layout(len16, n, 4, 0, blk, off, &end) == RNS_OK, "rns_packed_layout");
+    const uint64_t bytes = end + 16;
+    uint8_t *arena = malloc(bytes), *ref = malloc(bytes), *back = malloc(bytes);
+    fill_random(arena, bytes);
+    for (uint32_t i = 0; i < n; ++i) {
+        uint8_t *h = arena + off[i];
+        h[0] = 0x45; h[1] = 0; h[2] = (uint8_t)(len16[i] >> 8); h[3] = (uint8_t)len16[i];
+        h[6] = 0x40; h[7] = 0; h[8] = 64; h[9] = proto[i];
+        memcpy(h + 12, src, 4);
+        memcpy(h + 16, dst, 4);
+    }
+    memcpy(ref, arena, bytes);
+    for (uint32_t i = 0; i < n; ++i) {
+        uint8_t *h = ref + off[i], *seg = h + 20;
+        const uint32_t seglen = len16[i] - 20u, field = proto[i] == 6 ? 16u : proto[i] == 17 ? 6u : 2u;
+        h[10] = h[11] = 0;
+        const uint32_t ipc = (uint32_t)oracle_compute_checksum(h, 20);
+        h[10] = (uint8_t)(ipc >> 8); h[11] = (uint8_t)ipc;
+        seg[field] = seg[field + 1] = 0;
+        const int32_t ph = proto[i] == 1 ? 0 : oracle_compute_pseudo_header_checksum(src, 4, dst, 4, seglen, proto[i]);
+        const uint32_t l4 = 0xffffu ^ (uint32_t)oracle_compute_ones_comp((uint16_t)ph, seg, seglen);
+        seg[field] = (uint8_t)(l4 >> 8); seg[field + 1] = (uint8_t)l4;
+    }
+    uint8_t *d_arena, *d_status, *d_slots;
+    uint64_t *d_blk;
+    uint16_t *d_len16;
+    HIP_OK(hipMalloc((void **)&d_arena, bytes));
+    HIP_OK(hipMalloc((void **)&d_blk, ((n + 63) / 64) * sizeof *blk));
+    HIP_OK(hipMalloc((void **)&d_len16, n * sizeof *len16));
+    HIP_OK(hipMalloc((void **)&d_status, n));
+    HIP_OK(hipMalloc((void **)&d_slots, (uint64_t)n * 2048));
+    HIP_OK(hipMemcpy(d_arena, arena, bytes, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_blk, blk, ((n + 63) / 64) * sizeof *blk, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_len16, len16, n * sizeof *len16, hipMemcpyHostToDevice));
+    const uint32_t hints[2] = {0, 1500};
+    for (int h = 0; h < 2; ++h) {
+        HIP_OK(hipMemcpy(d_arena, arena, bytes, hipMemcpyHostToDevice));
+        CHECK(rns_tx_fill_packed_dev(d_arena, bytes, d_blk, d_len16, 4, n, d_status, hints[h], st) == RNS_OK,
+              "rns_tx_fill_packed_dev");
+        HIP_OK(hipStreamSynchronize(st));
+        HIP_OK(hipMemcpy(back, d_arena, bytes, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(status, d_status, n, hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < n; ++i)
+            CHECK(status[i] == (RNS_TX_IP_FILLED | RNS_TX_L4_FILLED), "packed tx (hint %u) status %u: %02x", hints[h],
+                  i, status[i]);
+        uint64_t diff = 0;
+        for (uint64_t b = 0; b < bytes; ++b)
+            diff += back[b] != ref[b];
+        CHECK(diff == 0, "packed tx (hint %u): %llu arena bytes differ from the oracle's", hints[h],
+              (unsigned long long)diff);
+    }
+    CHECK(rns_tx_fill_packed_dev(d_arena, bytes, d_blk, d_len16, 3, n, d_status, 0, st) == RNS_E_INVALID,
+          "align_log2 < 4 is invalid");
+    /* receive: the packed arena, then the datagrams in 2048-byte slots */
+    CHECK(rns_rx_verify_packed_dev(d_arena, bytes, d_blk, d_len16, 4, n, dst, dst6, d_status, NULL, st) == RNS_OK,
+          "rns_rx_verify_packed_dev");
+    HIP_OK(hipStreamSynchronize(st));
+    HIP_OK(hipMemcpy(status, d_status, n, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t want = RNS_RX_IP_OK | RNS_RX_ACCEPT | (proto[i] == 17 ? RNS_RX_L4_UNCHECKED : RNS_RX_L4_OK);
+        CHECK(status[i] == want, "packed rx status %u: %02x != %02x", i, status[i], want);
+    }
+    for (uint32_t i = 0; i < n; ++i)
+        HIP_OK(hipMemcpy(d_slots + (uint64_t)i * 2048, d_arena + off[i], len16[i], hipMemcpyDeviceToDevice));
+    CHECK(rns_rx_verify_strided_dev(d_slots, (uint64_t)n * 2048, 0, 2048, d_len16, n, dst, dst6, d_status, NULL, st) ==
+              RNS_OK, "rns_rx_verify_strided_dev");
+    HIP_OK(hipStreamSynchronize(st));
+    HIP_OK(hipMemcpy(status, d_status, n, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t want = RNS_RX_IP_OK | RNS_RX_ACCEPT | (proto[i] == 17 ? RNS_RX_L4_UNCHECKED : RNS_RX_L4_OK);
+        CHECK(status[i] == want, "strided rx status %u: %02x != %02x", i, status[i], want);
+    }
+    hipFree(d_arena); hipFree(d_blk); hipFree(d_len16); hipFree(d_status); hipFree(d_slots);
+    free(len16); free(off); free(blk); free(proto); free(status); free(arena); free(ref); free(back);
+    return 0;
+}
+
 int main(void)
 {
     const uint32_t n = 40000;
@@ -635,7 +730,8 @@ int main(void)
 
     /* 2b. the packed entry bench.py times, the fragment-chain entry, transmit finalize and
      *     receive verify: each against the oracle's util.rs restatement */
-    if (test_packed(st) || test_strided(st) || test_chains(st) || test_chain_fill(st) || test_chain_fill_txpacked(st) || test_tx_rx(st))
+    if (test_packed(st) || test_strided(st) || test_chains(st) || test_chain_fill(st) || test_chain_fill_txpacked(st) || test_tx_rx(st) ||
+        test_tx_rx_packed(st))
         return 2;
 
     /* 3. errors come back as status codes, never as aborts */

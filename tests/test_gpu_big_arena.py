@@ -9,8 +9,8 @@ translated), and for the in-place fills every byte of every window is compared.
 
 Entries covered: the packed checksum (rows kernel D = 8 and D = 16, the tiny rounds
 kernel, the unaligned-packing class kernel, a first block at an odd offset), the strided
-form, the packed and explicit transmit fills, packed and explicit receive verify, the
-transmit finalize, fragment chains (nontemporal and temporal class passes, each through a
+form, the packed and explicit transmit fills, packed, explicit and strided receive verify, the
+explicit and packed transmit finalize, fragment chains (nontemporal and temporal class passes, each through a
 buffer window based at its pass's fragments and through 64-bit loads for passes spanning more
 than 4 GiB; the runs hint, which is ignored past 4 GiB) and the head-fragment chain fill.  Reference: util.rs:88-119,
 tcp.rs:838-850 / 957-973, udp.rs:158-171, icmp.rs:46-112, ip.rs:76-80 / 158-159.
@@ -23,7 +23,7 @@ from oracle import oracle as O
 from rustnetworkstack_amd import _lib
 from rustnetworkstack_amd.batch import (csum_batch_packed, csum_batch_strided, csum_chain, csum_chain_fill,
                                         csum_fill, csum_fill_packed, fill_splitmix64, packed_layout, rx_verify,
-                                        rx_verify_packed, tx_fill)
+                                        rx_verify_packed, rx_verify_strided, tx_fill, tx_fill_packed)
 from test_gpu_rx import make_packets
 from test_gpu_tx import outgoing
 from test_rx_oracle import L4, L6, ipv4, tcp_seg, R4
@@ -328,6 +328,62 @@ def test_transmit_finalize(oracle, win):
         assert diff.size == 0, [(int(d), int(got[d]), int(want[d])) for d in diff[:8]]
     finally:
         win.restore()
+
+
+@pytest.mark.parametrize("hint", [0, 1500])
+def test_packed_transmit_finalize(oracle, win, hint):
+    """rns_tx_fill_packed_dev's BUF=false instantiations (D = 8 and 16): every kind of outgoing
+    datagram packed in each window (the middle one across the 4 GiB line, the last one at an
+    odd 16-byte offset: its units take the per-datagram path); every window byte and status
+    against oracle.tx_fill_ref."""
+    pk = [outgoing(640 + (9 if k == 2 else 0), 0x7C + k + hint) for k in range(3)]
+    lens = [np.array([len(p) for p in w], dtype=np.uint16) for w in pk]
+    blk, off, _, ln = packed_windows(win, lens, 4, shifts=(0, 16, 5))
+    cuts = np.cumsum([0] + [len(w) for w in pk])
+    try:
+        host = place(win, pk, [off[cuts[k]:cuts[k + 1]] for k in range(3)])
+        want_st = []
+        for k, w in enumerate(pk):
+            for o, p in zip(off[cuts[k]:cuts[k + 1]], w):
+                q, st = O.tx_fill_ref(p, ones_comp=oracle.compute_ones_comp)
+                r = int(o) - win.starts[k]
+                host[k][r:r + len(q)] = np.frombuffer(q, dtype=np.uint8)
+                want_st.append(st)
+        st = tx_fill_packed(win.arena, blk, dev(ln, np.int16), len_hint=hint)
+        torch.cuda.synchronize()
+        assert np.array_equal(st.cpu().numpy(), np.array(want_st, dtype=np.uint8))
+        got = np.concatenate(win.snapshot())
+        want = np.concatenate(host)
+        diff = np.flatnonzero(got != want)
+        assert diff.size == 0, [(int(d), int(got[d]), int(want[d])) for d in diff[:8]]
+    finally:
+        win.restore()
+
+
+@pytest.mark.parametrize("stride,shift", [(64, 0), (2048, 0), (2048, 3)])
+def test_strided_receive_verify(oracle, win, stride, shift):
+    """rns_rx_verify_strided_dev's BUF=false instantiation: a ring of slots in each window
+    (64-byte ACK slots: the quads' loads; 2048-byte MRU slots: the wave loop for the longer
+    datagrams; an unaligned first slot: the per-datagram path)."""
+    per = min(SPAN // stride - 2, 900)
+    for k in range(3):
+        pk = [p[:stride] for p in make_packets(per, 0x5C0 + k + stride)]
+        first = win.starts[k] + shift + (16 if k == 1 else 0)
+        if k == 1:  # the ring crosses the 4 GiB line
+            first = FOUR_G - stride * (per // 2) + shift
+        try:
+            place(win, [pk if j == k else [] for j in range(3)], [np.array([first + i * stride for i in range(per)],
+                                                                            dtype=np.uint64) if j == k else []
+                                                                  for j in range(3)])
+            ln = np.array([len(p) for p in pk], dtype=np.uint16)
+            want = [O.rx_verify_ref(p, L4, L6, ones_comp=oracle.compute_ones_comp) for p in pk]
+            l4 = torch.empty(per, dtype=torch.uint16, device=DEV)
+            st = rx_verify_strided(win.arena, stride, dev(ln, np.int16), L4, L6, first_off=first, l4_sum=l4)
+            torch.cuda.synchronize()
+            assert np.array_equal(st.cpu().numpy(), np.array([w[0] for w in want], dtype=np.uint8))
+            assert np.array_equal(host_u16(l4), np.array([w[1] for w in want], dtype=np.uint16))
+        finally:
+            win.restore()
 
 
 def chain_windows(win, per_window, salt, max_frag, min_head=1):

@@ -16,7 +16,11 @@ from test_rx_oracle import L4, L6
 pytestmark = pytest.mark.gpu
 
 
-def test_socket_to_verdicts(oracle):
+@pytest.mark.parametrize("packed", [True, False])
+def test_socket_to_verdicts(oracle, packed):
+    """Every kind of datagram through the synchronous receive: packed (rns_io_recv_batch_packed
+    -> the used bytes only -> rns_rx_verify_packed_dev) and in MRU slots (rns_rx_verify_dev);
+    verdicts, lengths and bytes against the reference's receive path."""
     pkts = make_packets(6000, 0xD1CE)
     lens = np.array([len(p) for p in pkts], dtype=np.uint32)
     off = np.zeros(len(pkts), dtype=np.uint64)
@@ -28,19 +32,26 @@ def test_socket_to_verdicts(oracle):
     a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_SEQPACKET)
     t = threading.Thread(target=send_batch, args=(a.fileno(), arena, off[nonempty], lens[nonempty]))
     t.start()
-    pipe = RxPipeline(L4, L6, device=0, max_pkts=1024)
-    got_st, got_len = [], []
+    pipe = RxPipeline(L4, L6, device=0, max_pkts=1024, packed=packed)
+    want = [p for p in pkts if len(p)]
+    got_st, got_len, bad_bytes = [], [], 0
     while sum(x.shape[0] for x in got_st) < int(nonempty.sum()):
         st, ln = pipe.receive(b.fileno(), timeout_ms=2000)
         assert st.shape[0] > 0, "receive timed out"
+        i0 = sum(x.shape[0] for x in got_st)
+        bad_bytes += sum(pipe.last[k].tobytes() != want[i0 + k] for k in range(ln.shape[0]))
         got_st.append(st)
         got_len.append(ln.copy())
     t.join()
+    h2d, n = pipe.h2d_bytes, pipe.datagrams
     pipe.close()
     a.close()
     b.close()
+    assert bad_bytes == 0
     assert np.array_equal(np.concatenate(got_len), lens[nonempty])
     assert np.array_equal(np.concatenate(got_st), expect)
+    pad = int(((lens[nonempty].astype(np.int64) + 15) // 16 * 16).sum())
+    assert h2d == (pad if packed else n * 2048)  # packed: the datagrams' padded bytes cross PCIe, not slots
 
 
 def test_tx_pipeline_to_socket(oracle):
@@ -84,7 +95,8 @@ def test_tx_pipeline_to_socket(oracle):
     assert not bad, bad[:5]
 
 
-def test_stream_overlapped(oracle):
+@pytest.mark.parametrize("packed", [True, False])
+def test_stream_overlapped(oracle, packed):
     """RxPipeline.stream: the host reads batch k+1 while batch k is verified; verdicts,
     lengths and slot bytes as the synchronous path would give them."""
     pkts = [p for p in make_packets(6000, 0x0BE1) if len(p) > 0]
@@ -96,13 +108,13 @@ def test_stream_overlapped(oracle):
     a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_SEQPACKET)
     t = threading.Thread(target=send_batch, args=(a.fileno(), arena, off, lens))
     t.start()
-    pipe = RxPipeline(L4, L6, device=0, max_pkts=512)
+    pipe = RxPipeline(L4, L6, device=0, max_pkts=512, packed=packed)
     got_st, got_len, bad_bytes, i = [], [], 0, 0
-    for st, ln, slots in pipe.stream(b.fileno(), timeout_ms=2000):
+    for st, ln, dg in pipe.stream(b.fileno(), timeout_ms=2000):
         got_st.append(st.copy())
         got_len.append(ln.copy())
         for k in range(ln.shape[0]):
-            bad_bytes += slots[k, : ln[k]].tobytes() != pkts[i + k]
+            bad_bytes += dg[k].tobytes() != pkts[i + k]
         i += ln.shape[0]
         if i >= len(pkts):
             break

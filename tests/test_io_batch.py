@@ -54,3 +54,69 @@ def test_timeout_and_max_pkts():
     assert b.getblocking()                                          # fd flags restored
     a.close()
     b.close()
+
+
+def test_packed_receive_layout_and_oversize_dropped():
+    """rns_io_recv_batch_packed (recvmmsg on a socket): every datagram at the next 16-byte
+    boundary, u16 lengths, one block offset per 64 datagrams, the bytes used; a datagram
+    longer than the MRU is dropped; the rest arrive in order, byte for byte."""
+    from rustnetworkstack_amd.batch import packed_layout, recv_batch_packed
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+    a.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 1 << 22)
+    b.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 22)
+    arena, off, lens = make(300, 7)
+    assert send_batch(a.fileno(), arena, off, lens) == 300
+    buf = np.full(2048 * 400, 0xEE, dtype=np.uint8)
+    ln, blk, end = recv_batch_packed(b.fileno(), buf, 2048, timeout_ms=1000)
+    keep = np.nonzero(lens <= 2048)[0]
+    assert 0 < keep.shape[0] < 300 and ln.shape[0] == keep.shape[0]
+    assert np.array_equal(ln.astype(np.uint32), lens[keep])
+    want_blk, want_off, want_end = packed_layout(ln.astype(np.uint32), 4, 0)
+    assert np.array_equal(blk, want_blk) and end == want_end
+    for j, i in enumerate(keep):
+        o, k = int(want_off[j]), int(ln[j])
+        assert np.array_equal(buf[o:o + k], arena[int(off[i]):int(off[i]) + k])
+    a.close()
+    b.close()
+
+
+def test_packed_receive_room_cap_and_timeout():
+    """The packed read stops while a full MRU datagram still fits, or at max_pkts; what is
+    left is read by the next call; nothing queued times out with 0."""
+    from rustnetworkstack_amd.batch import recv_batch_packed
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+    buf = np.zeros(4096, dtype=np.uint8)
+    ln, blk, end = recv_batch_packed(b.fileno(), buf, 2048, timeout_ms=10)
+    assert ln.shape[0] == 0 and end == 0
+    arena, off, lens = make(100, 11, maxlen=60)
+    send_batch(a.fileno(), arena, off, lens)
+    got = []
+    while len(got) < 100:
+        ln, blk, end = recv_batch_packed(b.fileno(), buf, 2048, max_pkts=70, timeout_ms=1000)
+        assert 0 < ln.shape[0] <= 70 and end <= buf.shape[0]
+        # every read stopped with room for one more MRU datagram behind the last one (or at max_pkts)
+        assert ln.shape[0] == 70 or end + 2048 > buf.shape[0] - 15 or len(got) + ln.shape[0] == 100
+        pos = 0
+        for k in ln:
+            got.append(buf[pos:pos + int(k)].tobytes())
+            pos = (pos + int(k) + 15) // 16 * 16
+    assert got == [arena[int(o):int(o) + int(n)].tobytes() for o, n in zip(off, lens)]
+    assert b.getblocking()
+    a.close()
+    b.close()
+
+
+def test_send_batch_large_batches_keep_order():
+    """sendmmsg in rounds of 64: 1000 datagrams arrive complete and in order."""
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+    a.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 1 << 23)
+    b.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 23)
+    arena, off, lens = make(1000, 13, maxlen=300)
+    assert send_batch(a.fileno(), arena, off, lens) == 1000
+    slots = np.zeros(512 * 1000, dtype=np.uint8)
+    o, ln = recv_batch(b.fileno(), slots, 512, timeout_ms=1000)
+    assert np.array_equal(ln, lens)
+    assert all(slots[512 * j:512 * j + int(n)].tobytes() == arena[int(off[j]):int(off[j]) + int(n)].tobytes()
+               for j, n in enumerate(ln))
+    a.close()
+    b.close()

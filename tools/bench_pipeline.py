@@ -1,9 +1,11 @@
 """End-to-end batched receive / transmit rates over a SOCK_SEQPACKET socketpair
 (TUN-like: one datagram per read / write).
 
-Receive (default): a sender thread writes N valid IPv4/TCP datagrams (1500 B); the
-receiver runs RxPipeline (rns_io_recv_batch into pinned 2048-B slots -> H2D -> fused
-rns_rx_verify_dev -> verdicts D2H) until all arrived.
+Receive (default): a sender thread writes N valid IPv4/TCP datagrams (1500 B, or 64 B
+with --config c2_64B; sendmmsg); the receiver runs RxPipeline until all arrived — packed
+(rns_io_recv_batch_packed: recvmmsg into a packed pinned arena -> H2D of the used bytes ->
+rns_rx_verify_packed_dev -> verdicts D2H), or with --slots the round-5 form (2048-B slots ->
+H2D of whole slots -> rns_rx_verify_dev).
 Transmit (--tx): the same datagrams with their checksum fields zeroed are placed in
 TxPipeline's pinned slots and sent (H2D -> rns_tx_fill_dev -> header bytes D2H ->
 rns_io_send_batch); a drain thread reads them and the result is spot-checked.
@@ -41,11 +43,13 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--tx", action="store_true")
     ap.add_argument("--overlap", action="store_true")
+    ap.add_argument("--slots", action="store_true", help="receive into 2048-B slots (round-5 form)")
+    ap.add_argument("--config", default="c3_1500B", help="datagram sizes: c3_1500B or c2_64B")
     args = ap.parse_args()
     if args.tx:
         return main_tx(args)
     dev = torch.device("cuda:0")
-    lay = make_layout("c3_1500B", n=args.packets)
+    lay = make_layout(args.config, n=args.packets)
     b = DeviceBatch(lay, dev)
     write_ipv4_tcp_headers(b, lay, dev)          # valid datagrams, built on the GPU
     arena = b.arena[:lay.arena_bytes].cpu().numpy()
@@ -53,7 +57,7 @@ def main():
     a, r = socket.socketpair(socket.AF_UNIX, socket.SOCK_SEQPACKET)
     for s_, opt in ((a, socket.SO_SNDBUF), (r, socket.SO_RCVBUF)):
         s_.setsockopt(socket.SOL_SOCKET, opt, 64 << 20)
-    pipe = RxPipeline(L4, L6, device=0, max_pkts=args.batch)
+    pipe = RxPipeline(L4, L6, device=0, max_pkts=args.batch, packed=not args.slots)
     sender = threading.Thread(target=send_batch, args=(a.fileno(), arena, lay.off, lay.length))
     t0 = time.perf_counter()
     sender.start()
@@ -74,11 +78,16 @@ def main():
         batches += 1
     dt = time.perf_counter() - t0
     sender.join()
-    res = {"packets": lay.n, "received": got, "accepted": accepted, "batches": batches,
-           "seconds": round(dt, 3), "packets_per_s": round(got / dt), "GBps": round(got * 1500 / dt / 1e9, 3),
-           "overlap": args.overlap,
-           "path": "AF_UNIX SOCK_SEQPACKET socketpair (TUN-like) -> rns_io_recv_batch (2048-B slots, pinned) -> "
-                   "H2D -> rns_rx_verify_dev -> status D2H; sender on another host thread"}
+    size = int(lay.length[0])
+    res = {"packets": lay.n, "datagram_bytes": size, "received": got, "accepted": accepted, "batches": batches,
+           "seconds": round(dt, 3), "packets_per_s": round(got / dt), "GBps": round(got * size / dt / 1e9, 3),
+           "h2d_bytes_per_datagram": round(pipe.h2d_bytes / max(pipe.datagrams, 1), 1),
+           "overlap": args.overlap, "packed": not args.slots,
+           "path": ("AF_UNIX SOCK_SEQPACKET socketpair (TUN-like; sendmmsg) -> " +
+                    ("rns_io_recv_batch (recvmmsg into 2048-B slots, pinned) -> H2D of whole slots -> rns_rx_verify_dev"
+                     if args.slots else
+                     "rns_io_recv_batch_packed (recvmmsg, 16-byte packing, pinned) -> H2D of the used bytes -> "
+                     "rns_rx_verify_packed_dev") + " -> status D2H; sender on another host thread")}
     print(json.dumps(res))
     if args.out:
         with open(args.out, "w") as f:

@@ -10,6 +10,8 @@
 //   read                 one wave per 64 packets streams their bytes (16 B/lane, 4 in flight)
 //   read+store{2,32}     the same, then each lane stores into one packet's field
 //   read+compact         the same, then one coalesced 128-B store of 64 u16 results
+//   read+store{64,128}   the same, each lane rewriting the whole aligned 64-B / 128-B block around its
+//                        packet's field (round 6: are full-block writes cheaper than partial ones?)
 //   read_xcd             read, with blocks renumbered so each XCD streams a contiguous eighth
 //   glds{4,8,16}         the slab through an LDS ring with global_load_lds (DEPTH-1 KB blocks in flight)
 #include <hip/hip_runtime.h>
@@ -54,6 +56,7 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nblk)
 }
 
 // MODE 0: read only; 1: + 2-byte field store; 2: + 32-byte sector store; 3: + compact u16 store
+// (MODE 7: + 64-byte block store; MODE 8: + 128-byte line store)
 // at the end of the wave's slab.  MODE 4: the lane that loaded a packet's field chunk
 // rewrites that 16-B chunk right after consuming it; MODE 5: the same store issued one
 // iteration later, after the next iteration's loads (so no load waits for it).
@@ -131,6 +134,12 @@ __global__ __launch_bounds__(256) void read_store(uint8_t *arena, uint32_t n, ui
         uint4 *q = reinterpret_cast<uint4 *>(arena + (f & ~31ull));
         q[0] = make_uint4(acc, acc, acc, acc);
         q[1] = make_uint4(acc, 0, acc, 0);
+    } else if constexpr (MODE == 7 || MODE == 8) {
+        constexpr uint32_t BS = MODE == 7 ? 64 : 128;
+        uint4 *q = reinterpret_cast<uint4 *>(arena + (f & ~static_cast<uint64_t>(BS - 1)));
+#pragma unroll
+        for (uint32_t k = 0; k < BS / 16; ++k)
+            q[k] = make_uint4(acc, k, acc, k);
     } else {
         out[p0 + lane] = static_cast<uint16_t>(acc);
     }
@@ -228,10 +237,15 @@ int main(int argc, char **argv)
         report("scatter16", time_ms([&] { scatter<16><<<sblocks, 256>>>(arena, n, stride, 7); }, iters));
         report("scatter32", time_ms([&] { scatter<32><<<sblocks, 256>>>(arena, n, stride, 7); }, iters));
         report("scatter64", time_ms([&] { scatter<64><<<sblocks, 256>>>(arena, n, stride, 7); }, iters));
+        report("scatter128", time_ms([&] { scatter<128><<<sblocks, 256>>>(arena, n, stride, 7); }, iters));
         report("read", time_ms([&] { read_store<0><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
         report("read+store2", time_ms([&] { read_store<1><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
         report("read+store32", time_ms([&] { read_store<2><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
         report("read+compact", time_ms([&] { read_store<3><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read+store64", time_ms([&] { read_store<7><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read+store128", time_ms([&] { read_store<8><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read_plain+store2", time_ms([&] { read_store<1, 0><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
+        report("read_plain+store64", time_ms([&] { read_store<7, 0><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
         report("read+dep_desc", time_ms([&] { read_store<6><<<rblocks, 256>>>(arena, n, stride, out); }, iters));
         // occupancy capped by dynamic LDS per 4-wave workgroup (160 KB per CU)
         report("read_occ4", time_ms([&] { read_store<0><<<rblocks, 256, 40 << 10>>>(arena, n, stride, out); }, iters));
