@@ -745,6 +745,10 @@ __device__ __forceinline__ void store_field(const CsumArgs &a, __amdgpu_buffer_r
     }
 }
 
+// (Rewriting each field's whole 64-byte memory segment from the owner's chunks where the segment
+// lies inside the datagram — full-segment writes instead of partial ones, which the store probe
+// measured cheaper on cold lines — was slower: c3 322.6-323.0 / IMIX 823.4-826.7 us against
+// 305.8-306.6 / 810.7-812.8, parity green; it reloads chunks 3-5 after the rows: session r06e.)
 template <bool NT, bool BUF, int D>
 __global__ __launch_bounds__(64, D >= 16 ? 4 : RNS_ROWS_TX_OCC) void csum_rows_tx_kernel(const CsumArgs a)
 {
@@ -786,7 +790,9 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : RNS_ROWS_TX_OCC) void csum_rows_t
     };
     if ((r0 & 15) == 0) {
         uint4 own[kNS];
-        own[3] = own[4] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int i = 3; i < kNS; ++i)
+            own[i] = make_uint4(0, 0, 0, 0);
         if (!__ballot(len > 64)) {
             // ---- ACK-sized unit: every owner takes its datagram whole ----
 #pragma unroll
@@ -840,11 +846,11 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : RNS_ROWS_TX_OCC) void csum_rows_t
         // 81-96 bytes)
         const uint64_t b0 = start & ~15ull;
         const uint32_t s0 = static_cast<uint32_t>(start & 15);
-        uint4 own[kNS + 1];
+        uint4 own[6];
 #pragma unroll
-        for (int i = 0; i < kNS + 1; ++i)
+        for (int i = 0; i < 6; ++i)
             own[i] = own_chunk<BUF>(a, rsrc, recs, b0, present ? s0 + len : 0u, i);
-        st = tx_finish<kNS + 1>(own, mine, s0, len, start & 1, present, fld, val);
+        st = tx_finish<6>(own, mine, s0, len, start & 1, present, fld, val);
     }
     // (after the wave's loads: a store between a load and its use would join the in-order
     // vmcnt queue)

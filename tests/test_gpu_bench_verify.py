@@ -20,8 +20,9 @@ def test_bench_verify_rejects_exactly_the_corrupted(config, steps):
     assert v["rejected_total"] == v["rejected_expected"]
     assert v["datagrams_total"] > 0
     assert line["metric"] == bench.METRIC_VERIFY
-    # packed receive arenas: the rows receive kernel, or for ACK-sized datagrams (c2) the stream kernel
-    want = "csum_stream_kernel" if config == "c2_64B" else "csum_rows_rx_kernel"
+    # packed receive arenas: the rows receive kernel; c2's 64-byte datagrams in 64-byte slots: the
+    # strided receive kernel (rns_rx_verify_strided_dev)
+    want = "csum_strided_rx_kernel" if config == "c2_64B" else "csum_rows_rx_kernel"
     assert line["roofline"]["kernel"].startswith(want)
     assert 0 < line["roofline"]["frac"] < 1.0
     assert line["cpu_baseline"] is None

@@ -116,6 +116,83 @@ def test_garbage_datagrams_match_reference_receive_path(oracle, seed):
     assert not bad, bad[:5]
 
 
+def garbage_datagrams(seed, n, maxlen=3000):
+    """Random bytes as datagrams: a third version 4 (random IHL), a third version 6, the rest
+    anything; lengths 0..maxlen-1."""
+    w = O.splitmix64_words(0x6A4C + seed, 2 * n)
+    pkts = []
+    for i in range(n):
+        L = int(w[2 * i] % np.uint64(maxlen))
+        p = bytearray(O.splitmix64_bytes(int(w[2 * i + 1]), L).tobytes())
+        if L and i % 3 == 0:
+            p[0] = 0x40 | (p[0] & 0x0F)
+        elif L and i % 3 == 1:
+            p[0] = 0x60 | (p[0] & 0x0F)
+        pkts.append(bytes(p))
+    return pkts
+
+
+@pytest.mark.parametrize("seed", SEEDS[:1] if "RNS_FUZZ_SEEDS" not in os.environ else SEEDS)
+def test_garbage_datagrams_packed_and_strided_receive(oracle, seed):
+    """The same garbage through the packed receive entry (rows receive kernel, 16-byte packing)
+    and the strided one (2048-byte slots and 64-byte slots holding datagrams of at most 64 B):
+    status and L4 sum against the reference's receive path."""
+    from rustnetworkstack_amd.batch import packed_layout, rx_verify_packed, rx_verify_strided
+    pkts = garbage_datagrams(seed, 5000, 2048)
+    want = [O.rx_verify_ref(p, L4, L6, ones_comp=oracle.compute_ones_comp) for p in pkts]
+    ln = np.array([len(p) for p in pkts], dtype=np.uint16)
+    blk, poff, end = packed_layout(ln, 4, 0)
+    arena = np.full(end + 16, 0x5A, dtype=np.uint8)
+    slots = np.full(2048 * len(pkts), 0xA5, dtype=np.uint8)
+    for i, (o, p) in enumerate(zip(poff.tolist(), pkts)):
+        arena[o:o + len(p)] = np.frombuffer(p, dtype=np.uint8)
+        slots[2048 * i:2048 * i + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    for name, run in (("packed", lambda l4: rx_verify_packed(torch.from_numpy(arena).to(DEV), dev(blk, np.int64),
+                                                             dev(ln, np.int16), L4, L6, l4_sum=l4)),
+                      ("strided", lambda l4: rx_verify_strided(torch.from_numpy(slots).to(DEV), 2048,
+                                                               dev(ln, np.int16), L4, L6, l4_sum=l4))):
+        l4 = torch.empty(len(pkts), dtype=torch.uint16, device=DEV)
+        st = run(l4)
+        got = list(zip(st.cpu().numpy().tolist(), host_u16(l4).tolist()))
+        bad = [(i, len(pkts[i]), got[i], want[i]) for i in range(len(pkts)) if got[i] != tuple(want[i])]
+        assert not bad, (name, bad[:5])
+    tiny = [p[:64] for p in pkts]
+    want = [O.rx_verify_ref(p, L4, L6, ones_comp=oracle.compute_ones_comp) for p in tiny]
+    ring = np.full(64 * len(tiny), 0xA5, dtype=np.uint8)
+    for i, p in enumerate(tiny):
+        ring[64 * i:64 * i + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    l4 = torch.empty(len(tiny), dtype=torch.uint16, device=DEV)
+    st = rx_verify_strided(torch.from_numpy(ring).to(DEV), 64, dev(np.array([len(p) for p in tiny], np.uint16),
+                                                                     np.int16), L4, L6, l4_sum=l4)
+    got = list(zip(st.cpu().numpy().tolist(), host_u16(l4).tolist()))
+    bad = [(i, got[i], want[i]) for i in range(len(tiny)) if got[i] != tuple(want[i])]
+    assert not bad, ("64-byte slots", bad[:5])
+
+
+@pytest.mark.parametrize("seed", SEEDS[:1] if "RNS_FUZZ_SEEDS" not in os.environ else SEEDS)
+def test_garbage_datagrams_packed_transmit(oracle, seed):
+    """Garbage as outgoing datagrams through the packed transmit finalize: every arena byte and
+    status against the reference's transmit path (oracle.tx_fill_ref)."""
+    from rustnetworkstack_amd.batch import packed_layout, tx_fill_packed
+    pkts = garbage_datagrams(seed + 100, 5000, 2048)
+    ln = np.array([len(p) for p in pkts], dtype=np.uint16)
+    blk, poff, end = packed_layout(ln, 4, 0)
+    arena = O.splitmix64_bytes(0x7A0 + seed, end + 32)
+    want = arena.copy()
+    want_st = np.zeros(len(pkts), dtype=np.uint8)
+    for i, (o, p) in enumerate(zip(poff.tolist(), pkts)):
+        arena[o:o + len(p)] = np.frombuffer(p, dtype=np.uint8)
+        q, st_ = O.tx_fill_ref(p, ones_comp=oracle.compute_ones_comp)
+        want[o:o + len(q)] = np.frombuffer(q, dtype=np.uint8)
+        want_st[i] = st_
+    a = torch.from_numpy(arena).to(DEV)
+    st = tx_fill_packed(a, dev(blk, np.int64), dev(ln, np.int16)).cpu().numpy()
+    assert np.array_equal(st, want_st), np.flatnonzero(st != want_st)[:5]
+    got = a.cpu().numpy()
+    diff = np.flatnonzero(got != want)
+    assert diff.size == 0, [(int(d), int(got[d]), int(want[d])) for d in diff[:8]]
+
+
 def test_host_batches_from_concurrent_threads(oracle):
     """One staging context per thread, as the receive, timer and application threads
     of the stack would hold; the C calls release the GIL."""
