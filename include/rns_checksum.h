@@ -141,7 +141,8 @@ int rns_packed_layout(const uint16_t *len16, uint64_t n, uint32_t align_log2, ui
                       uint64_t *off, uint64_t *end);
 
 /* Same, for packets at a fixed stride (no offset/length arrays to read):
- * packet i = d_arena[first_off + i*stride .. + len). */
+ * packet i = d_arena[first_off + i*stride .. + len).  Offsets that would wrap 64 bits are
+ * RNS_E_INVALID (also for rns_rx_verify_strided_dev). */
 int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uint64_t first_off,
                                uint64_t stride, uint32_t len, const uint16_t *d_seed, uint16_t *d_out,
                                uint32_t n, uint32_t flags, uint32_t *d_bad, void *stream);

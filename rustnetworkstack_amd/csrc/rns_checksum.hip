@@ -97,6 +97,14 @@ int drain_slot(rns_host_ctx::Slot &s, uint16_t *h_out)
 
 }  // namespace
 
+// A strided call's offsets first_off + i * stride (+ the base adjustment) must not wrap 64 bits:
+// a wrapped offset would name bytes inside the arena that are not packet i's.
+static bool strided_fits(uint64_t first_off, uint64_t stride, uint32_t n)
+{
+    const uint64_t room = ~0ull - 16u - first_off;
+    return first_off <= ~0ull - 16u && (n <= 1 || stride <= room / (n - 1));
+}
+
 extern "C" {
 
 int rns_csum_batch_dev_cfg(const uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off,
@@ -188,7 +196,7 @@ int rns_csum_batch_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uin
 {
     if (n == 0)
         return RNS_OK;
-    if (!d_arena || !d_out)
+    if (!d_arena || !d_out || !strided_fits(first_off, stride, n))
         return RNS_E_INVALID;
     if (int st = check_device())
         return st;
@@ -440,7 +448,7 @@ int rns_rx_verify_strided_dev(const uint8_t *d_arena, uint64_t arena_bytes, uint
 {
     if (n == 0)
         return RNS_OK;
-    if (!d_arena || !d_len16 || !d_status || !local_ipv4 || !local_ipv6)
+    if (!d_arena || !d_len16 || !d_status || !local_ipv4 || !local_ipv6 || !strided_fits(first_off, stride, n))
         return RNS_E_INVALID;
     if (int st = check_device())
         return st;

@@ -67,6 +67,29 @@ def test_batch_calls_fail_loudly_without_gpu():
                                         None) == _lib.RNS_E_NODEVICE
     assert lib.rns_rx_verify_dev(fake, 64, fake, fake, 1, fake, fake, fake, None, None) == _lib.RNS_E_NODEVICE
     assert lib.rns_tx_fill_dev(fake, 64, fake, fake, 1, None, None) == _lib.RNS_E_NODEVICE
+    assert lib.rns_tx_fill_packed_dev(fake, 64, fake, fake, 4, 1, None, 0, None) == _lib.RNS_E_NODEVICE
+    assert lib.rns_rx_verify_strided_dev(fake, 64, 0, 64, fake, 1, fake, fake, fake, None,
+                                         None) == _lib.RNS_E_NODEVICE
+
+
+def test_argument_errors_before_the_device():
+    """Bad arguments are reported as RNS_E_INVALID before any device call (no GPU needed):
+    strided offsets that would wrap 64 bits, a packed finalize below 16-byte alignment, a
+    packed receive into an MRU of more than 65535 bytes."""
+    lib = _lib.load()
+    fake = ctypes.c_void_p(4096)
+    out = ctypes.c_uint16()
+    big = (1 << 63) + 16
+    assert lib.rns_csum_batch_strided_dev(fake, 64, 0, big, 64, None, ctypes.addressof(out), 3, 0, None,
+                                          None) == _lib.RNS_E_INVALID
+    assert lib.rns_csum_batch_strided_dev(fake, 64, (1 << 64) - 8, 16, 64, None, ctypes.addressof(out), 1, 0, None,
+                                          None) == _lib.RNS_E_INVALID
+    assert lib.rns_rx_verify_strided_dev(fake, 64, 0, big, fake, 3, fake, fake, fake, None,
+                                         None) == _lib.RNS_E_INVALID
+    assert lib.rns_tx_fill_packed_dev(fake, 64, fake, fake, 3, 1, None, 0, None) == _lib.RNS_E_INVALID
+    end = ctypes.c_uint64()
+    assert lib.rns_io_recv_batch_packed(0, fake, 4096, 70000, 4, fake, fake, ctypes.byref(end), 0) == \
+        _lib.RNS_E_INVALID
 
 
 def test_python_batch_api_refuses_cpu_tensors():
