@@ -308,6 +308,28 @@ int rns_tx_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_of
 int rns_tx_fill_packed_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_blk_off, const uint16_t *d_len16,
                            uint32_t align_log2, uint32_t n, uint8_t *d_status, uint32_t len_hint, void *stream);
 
+/* Transmit finalize of datagrams held as NetBuffer chains — the reference's own transmit layout
+ * (buf.rs:262-291, 385-420): datagram i = the CSR chain of rns_csum_chain_dev (fragments
+ * [d_first[i], d_first[i+1]) of (d_frag_off, d_frag_len)), whose FIRST fragment is the head
+ * fragment alloc_header built — the IP header and, behind it, the L4 header (both prepended
+ * into one fragment) — followed by the payload fragments.  Per datagram what tcp_output /
+ * udp_output / icmp_output_* and ip_output_v4 store (tcp.rs:957-973, udp.rs:151-171,
+ * icmp.rs:87-112, ip.rs:140-160): the L4 checksum = compute_buffer_ones_comp(pseudo-header,
+ * [head[hdr..], payload...]) folded per fragment as the reference folds it (an odd-length
+ * fragment pads its last byte), pseudo-header from the head's addresses and the chain's total
+ * length; the IPv4 header checksum over head[..IHL*4]; both fields computed as zero and stored
+ * big-endian into the head fragment.  Only head bytes are written.  d_status (optional) gets
+ * RNS_TX_*: MALFORMED (untouched) for a malformed range, no fragments, a fragment outside the
+ * arena, or a head that does not hold the IP header; no L4 fill for a protocol the stack does
+ * not checksum, a segment too short for its field, or a field past the head fragment.  Heads
+ * of consecutive datagrams back to back in a header region and payloads back to back at
+ * 16-byte-aligned starts (the shape of RNS_FLAG_CHAIN_TX_PACKED; heads of at most 80 bytes from
+ * their 16-byte boundary, at most 4 payload fragments forming a run) stream as rows; any other
+ * 64-datagram block takes an exact per-datagram loop (same results, slower).  n_pkts >
+ * RNS_CHAIN_MAX_PACKETS is RNS_E_INVALID. */
+int rns_tx_fill_chain_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_frag_off, const uint32_t *d_frag_len,
+                          uint32_t n_frags, const uint32_t *d_first, uint32_t n_pkts, uint8_t *d_status, void *stream);
+
 /* Tuning entry (bench / tests): explicit kernel shape.  variant bit 0: 0 = group
  * kernel (one lane stores each result), 1 = rounds kernel (a wave owns 64
  * consecutive packets, one coalesced result store); bit 1: nontemporal packet

@@ -218,6 +218,66 @@ def tx_fill_ref(pkt: bytes, ones_comp=None) -> tuple:
     return bytes(p), st
 
 
+def tx_chain_fill_ref(frags, ones_comp=None) -> tuple:
+    """(head fragment bytes, status bits) after the reference's transmit path has filled the
+    checksums of one datagram held as a NetBuffer chain: frags[0] is the head fragment, where
+    alloc_header leaves the L4 header and then, prepended into the same fragment's headroom,
+    the IP header (buf.rs:262-291: a header is always contiguous); frags[1:] are the payload
+    fragments.  The L4 checksum is compute_buffer_ones_comp(pseudo-header, packet) taken when
+    the packet was [head[hdr:], payload...] (tcp.rs:957-973, udp.rs:150-171,
+    icmp.rs:87-112): folded per fragment (util.rs:112-119), so an odd-length fragment pairs
+    its bytes from its own start; the IPv4 header checksum covers head[:IHL*4] (ip.rs:140-160).
+    Fields count as zero, as alloc_header leaves them.  Only head bytes change.  A chain whose
+    head cannot hold its IP header (or no fragments / bad version) is TX_MALFORMED and left
+    unchanged; an L4 field outside the head fragment, or a protocol the stack does not
+    checksum, gets no L4 fill.  Empty payload fragments add nothing (the reference would
+    panic, util.rs:92)."""
+    oc = ones_comp or ones_comp_py
+    if not frags or len(frags[0]) == 0:
+        return (bytes(frags[0]) if frags else b""), TX_MALFORMED
+    head = bytearray(frags[0])
+    hl = len(head)
+    L = sum(len(f) for f in frags)
+    version = head[0] >> 4
+    if version == 4:
+        hdr = (head[0] & 0xF) * 4
+        if hdr < 20 or hdr > hl:
+            return bytes(head), TX_MALFORMED
+        proto, src, dst = head[9], bytes(head[12:16]), bytes(head[16:20])
+    elif version == 6:
+        hdr = 40
+        if hl < 40:
+            return bytes(head), TX_MALFORMED
+        proto, src, dst = head[6], bytes(head[8:24]), bytes(head[24:40])
+    else:
+        return bytes(head), TX_MALFORMED
+    seg_len = L - hdr
+    field, seed = None, 0
+    if proto == 6:
+        field, seed = 16, pseudo_header_py(src, dst, seg_len & 0xFFFF, 6)
+    elif proto == 17:
+        field, seed = 6, pseudo_header_py(src, dst, seg_len & 0xFFFF, 17)
+    elif proto == 1 and version == 4:
+        field = 2
+    elif proto == 58 and version == 6:
+        field, seed = 2, pseudo_header_py(src, dst, seg_len, 58)
+    st = 0
+    if field is not None and seg_len >= field + 2 and hdr + field + 2 <= hl:
+        f = hdr + field
+        head[f:f + 2] = b"\x00\x00"
+        acc = seed
+        for piece in [bytes(head[hdr:])] + [bytes(x) for x in frags[1:]]:
+            if len(piece):
+                acc = oc(acc, piece)
+        head[f:f + 2] = (acc ^ 0xFFFF).to_bytes(2, "big")
+        st |= TX_L4_FILLED
+    if version == 4:
+        head[10:12] = b"\x00\x00"
+        head[10:12] = (oc(0, bytes(head[:hdr])) ^ 0xFFFF).to_bytes(2, "big")
+        st |= TX_IP_FILLED
+    return bytes(head), st
+
+
 # --------------------------------------------------------------------------
 # deterministic synthetic bytes: splitmix64 (SURVEY §8d, seed 0x5EED_C0DE)
 # --------------------------------------------------------------------------

@@ -60,6 +60,7 @@ EXPORTED_SYMBOLS = (
     "rns_rx_verify_strided_dev",
     "rns_tx_fill_dev",
     "rns_tx_fill_packed_dev",
+    "rns_tx_fill_chain_dev",
     "rns_host_ctx_create",
     "rns_host_ctx_destroy",
     "rns_csum_batch_host",
@@ -137,6 +138,7 @@ _SIGNATURES = {
     "rns_rx_verify_strided_dev": (_int, [_vp, _u64, _u64, _u64, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),
     "rns_tx_fill_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _vp]),
     "rns_tx_fill_packed_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _u32, _vp, _u32, _vp]),
+    "rns_tx_fill_chain_dev": (_int, [_vp, _u64, _vp, _vp, _u32, _vp, _u32, _vp, _vp]),
     "rns_host_ctx_create": (_int, [_int, _u64, _u32, ctypes.POINTER(_vp)]),
     "rns_host_ctx_destroy": (_int, [_vp]),
     "rns_csum_batch_host": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _vp, _u32, _u32]),

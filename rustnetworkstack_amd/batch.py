@@ -587,6 +587,42 @@ def tx_fill_packed(arena: torch.Tensor, blk_off: torch.Tensor, len16: torch.Tens
     return status
 
 
+def tx_fill_chain(arena: torch.Tensor, frag_off: torch.Tensor, frag_len: torch.Tensor, first: torch.Tensor, *,
+                  status: torch.Tensor | None = None) -> torch.Tensor:
+    """Transmit finalize of datagrams held as NetBuffer chains (rns_tx_fill_chain_dev):
+    datagram i = fragments ``first[i] .. first[i+1]`` as for ``csum_chain``, its FIRST
+    fragment the head alloc_header built (the IP header, then the L4 header: buf.rs:262-291),
+    the rest its payload.  The L4 checksum over [head[hdr:], payload...] (folded per fragment,
+    tcp.rs:957-973, udp.rs:151-171, icmp.rs:87-112) and the IPv4 header checksum
+    (ip.rs:140-160) are stored into the head.  Returns a uint8 status per datagram (RNS_TX_*)."""
+    _require_cuda(arena, "arena", (torch.uint8,))
+    _require_cuda(frag_off, "frag_off", (torch.int64,))
+    _require_cuda(frag_len, "frag_len", (torch.int32,))
+    _require_cuda(first, "first", (torch.int32,))
+    nf = frag_off.numel()
+    n = first.numel() - 1
+    if frag_len.numel() != nf or n < 0:
+        raise ValueError("frag_off/frag_len sizes differ or first is empty")
+    if n > _lib.RNS_CHAIN_MAX_PACKETS or nf >= 2 ** 32:
+        raise ValueError(f"at most {_lib.RNS_CHAIN_MAX_PACKETS} datagrams and 2^32-1 fragments per chain call")
+    dev = arena.device
+    for name, t in (("frag_off", frag_off), ("frag_len", frag_len), ("first", first)):
+        if t.device != dev:
+            raise ValueError(f"{name} is on {t.device}, arena on {dev}")
+    if status is None:
+        status = torch.empty(n, dtype=torch.uint8, device=dev)
+    else:
+        _require_cuda(status, "status", (torch.uint8,))
+        if status.numel() != n or status.device != dev:
+            raise ValueError(f"status must be {n} uint8 entries on {dev}")
+    with torch.cuda.device(dev):
+        st = _lib.load().rns_tx_fill_chain_dev(arena.data_ptr(), arena.numel(), frag_off.data_ptr(),
+                                              frag_len.data_ptr(), nf, first.data_ptr(), n, status.data_ptr(),
+                                              _stream_handle(dev))
+    _lib.check(st, "rns_tx_fill_chain_dev")
+    return status
+
+
 def tx_fill(arena: torch.Tensor, off: torch.Tensor, length: torch.Tensor, *,
             status: torch.Tensor | None = None) -> torch.Tensor:
     """Transmit finalize of a batch of outgoing IP datagrams (rns_tx_fill_dev): the

@@ -56,6 +56,19 @@ int launch_txrows(const CsumArgs &a, hipStream_t st)
     return hip_status(hipGetLastError());
 }
 
+// Transmit finalize of chains (rns_tx_fill_chain_dev): the transmit-rows kernel in FIN mode, whatever the
+// batch's shape (a wave without the transmit-packed shape takes its exact per-packet loop).
+int launch_txfin(const CsumArgs &a, hipStream_t st)
+{
+    constexpr bool NT = RNS_STREAM_NT != 0;
+    const dim3 grid(static_cast<uint32_t>((static_cast<uint64_t>(a.n) + 63) / 64)), block(64);
+    if (buf_records(a) < kOobOffset)
+        hipLaunchKernelGGL((csum_txrows_kernel<NT, true, RNS_TXROWS_D, false, true>), grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL((csum_txrows_kernel<NT, false, RNS_TXROWS_D, false, true>), grid, block, 0, st, a);
+    return hip_status(hipGetLastError());
+}
+
 template int launch_chain<false>(const CsumArgs &, uint32_t, bool, bool, hipStream_t);
 template int launch_chain<true>(const CsumArgs &, uint32_t, bool, bool, hipStream_t);
 template int launch_txrows<false>(const CsumArgs &, hipStream_t);

@@ -487,6 +487,27 @@ int rns_tx_fill_packed_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_
     return launch_tx_packed(a, static_cast<hipStream_t>(stream));
 }
 
+int rns_tx_fill_chain_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_frag_off, const uint32_t *d_frag_len,
+                          uint32_t n_frags, const uint32_t *d_first, uint32_t n_pkts, uint8_t *d_status, void *stream)
+{
+    if (n_pkts == 0)
+        return RNS_OK;
+    if (!d_arena || !d_first || (n_frags && (!d_frag_off || !d_frag_len)) || n_pkts > RNS_CHAIN_MAX_PACKETS)
+        return RNS_E_INVALID;
+    if (int st = check_device())
+        return st;
+    CsumArgs a{};
+    set_arena(a, d_arena, arena_bytes);
+    a.off = d_frag_off;
+    a.len = d_frag_len;
+    a.first = d_first;
+    a.n_frags = n_frags;
+    a.n = n_pkts;
+    a.flags = RNS_FLAG_COMPLEMENT;
+    a.status = d_status;
+    return launch_txfin(a, static_cast<hipStream_t>(stream));
+}
+
 int rns_tx_fill_dev(uint8_t *d_arena, uint64_t arena_bytes, const uint64_t *d_off, const uint32_t *d_len,
                     uint32_t n, uint8_t *d_status, void *stream)
 {

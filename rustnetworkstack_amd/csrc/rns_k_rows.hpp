@@ -662,6 +662,51 @@ __device__ __forceinline__ void head40(const uint4 (&ch)[NS], uint32_t s, uint32
     }
 }
 
+// The transmit path's reading of a datagram of L bytes whose first 40 bytes are h (head40)
+// and whose IP header must lie within its first hl bytes: the IP header length, the L4 field
+// (offset after the IP header: TCP 16, UDP 6, ICMPv4 / ICMPv6 2; kNoField for a protocol the
+// stack does not checksum) and the pseudo-header sum the L4 output routine seeds with
+// (tcp.rs:957-966, udp.rs:158-165, icmp.rs:97-104; none for ICMPv4, icmp.rs:87-95).  False:
+// a datagram the stack cannot produce (bad version, IHL < 5, header past hl).
+__device__ __forceinline__ bool tx_parse(const uint32_t (&h)[10], uint32_t L, uint32_t hl, uint32_t &hdr,
+                                         uint32_t &field, uint32_t &seed, bool &v4)
+{
+    const uint32_t b0 = h[0] & 0xffu, version = b0 >> 4;
+    uint32_t proto, addr;  // addr: BE word sum of source + destination (tcp.rs:958-966)
+    if (version == 4) {
+        hdr = (b0 & 15u) * 4u;
+        if (hdr < 20 || hdr > hl)
+            return false;
+        proto = (h[2] >> 8) & 0xffu;            // header[9]
+        addr = be2(h[3]) + be2(h[4]);            // header[12..20]
+    } else if (version == 6) {
+        hdr = 40;
+        if (hl < 40)
+            return false;
+        proto = (h[1] >> 16) & 0xffu;           // header[6]
+        addr = 0;
+#pragma unroll
+        for (int k = 2; k < 10; ++k)             // header[8..40]
+            addr += be2(h[k]);
+    } else {
+        return false;
+    }
+    v4 = version == 4;
+    const uint32_t seg = L - hdr, l16 = seg & 0xffffu;  // packet.len() as u16 (tcp.rs:942, udp.rs:152)
+    field = kNoField;
+    seed = 0;
+    if (proto == 6 || proto == 17) {
+        field = proto == 6 ? 16u : 6u;
+        seed = fold16(addr + proto + l16);
+    } else if (proto == 1 && v4) {
+        field = 2;  // icmp_output_v4: no pseudo-header
+    } else if (proto == 58 && !v4) {
+        field = 2;  // icmp_output_v6: full length, protocol 58
+        seed = fold16(addr + 58 + (seg >> 16) + (seg & 0xffffu));
+    }
+    return true;
+}
+
 // Owner-lane finish of transmit finalize for one datagram of L bytes: ch = its chunks from
 // the 16-byte boundary at or below its start (raw memory bytes; s = start & 15; NS chunks
 // hold bytes up to s + 78: the TCP field behind a 60-byte IPv4 header), mine = the
@@ -680,41 +725,15 @@ __device__ __forceinline__ uint8_t tx_finish(const uint4 (&ch)[NS], uint32_t min
         return RNS_TX_MALFORMED;
     uint32_t h[10];
     head40(ch, s, h);
-    const uint32_t b0 = h[0] & 0xffu, version = b0 >> 4;
-    uint32_t hdr, proto, addr;  // addr: BE word sum of source + destination (tcp.rs:958-966)
-    if (version == 4) {
-        hdr = (b0 & 15u) * 4u;
-        if (hdr < 20 || hdr > L)
-            return RNS_TX_MALFORMED;
-        proto = (h[2] >> 8) & 0xffu;            // header[9]
-        addr = be2(h[3]) + be2(h[4]);            // header[12..20]
-    } else if (version == 6) {
-        hdr = 40;
-        if (L < 40)
-            return RNS_TX_MALFORMED;
-        proto = (h[1] >> 16) & 0xffu;           // header[6]
-        addr = 0;
-#pragma unroll
-        for (int k = 2; k < 10; ++k)             // header[8..40]
-            addr += be2(h[k]);
-    } else {
+    uint32_t hdr, field, seed;
+    bool v4;
+    if (!tx_parse(h, L, L, hdr, field, seed, v4))
         return RNS_TX_MALFORMED;
-    }
-    const uint32_t seg = L - hdr, l16 = seg & 0xffffu;  // packet.len() as u16 (tcp.rs:942, udp.rs:152)
-    uint32_t field = kNoField, seed = 0;
-    if (proto == 6 || proto == 17) {
-        field = proto == 6 ? 16u : 6u;
-        seed = fold16(addr + proto + l16);
-    } else if (proto == 1 && version == 4) {
-        field = 2;  // icmp_output_v4: no pseudo-header
-    } else if (proto == 58 && version == 6) {
-        field = 2;  // icmp_output_v6: full length, protocol 58
-        seed = fold16(addr + 58 + (seg >> 16) + (seg & 0xffffu));
-    }
+    const uint32_t seg = L - hdr;
     const int lo = static_cast<int>(s);
     const uint32_t H = stash_sum_le(ch, lo, lo + static_cast<int>(hdr));
     uint8_t st = 0;
-    if (version == 4) {  // compute_checksum(header) with header[10..12] as zero
+    if (v4) {  // compute_checksum(header) with header[10..12] as zero
         fld[0] = 10;
         val[0] = finalize_bits(H - stash_sum_le(ch, lo + 10, lo + 12), odd, false, 0u, true, RNS_FLAG_COMPLEMENT);
         st |= RNS_TX_IP_FILLED;
@@ -729,8 +748,53 @@ __device__ __forceinline__ uint8_t tx_finish(const uint4 (&ch)[NS], uint32_t min
     return st;
 }
 
-// set_be16 of a finished field at absolute arena offset fp (util.rs:132-135)
-template <bool BUF>
+// The head fragment's part of a chain's transmit finalize (csum_txrows_kernel FIN mode): ch =
+// the head's chunks from the 16-byte boundary at or below its start (s = start & 15), hl = its
+// length (the IP header and, behind it, the L4 header: alloc_header prepends both into one
+// fragment, buf.rs:262-291), L = the datagram's length over every fragment.  ipv = the IPv4
+// header checksum to store at head + 10 (ip.rs:140-160); l4f = the L4 field's offset in the
+// head (kNoField: no L4 fill — a protocol the stack does not checksum, a segment too short
+// for its field, or a field past the head fragment); hsum = the LE word sum of the head's L4
+// part with the field as zero (valid when s + hl <= 16 * NS); seed = the pseudo-header sum.
+// The L4 part starts at an even distance from the head's start (IHL*4 or 40), so hsum pairs
+// exactly as that part would alone.
+template <int NS>
+__device__ __forceinline__ uint8_t chain_tx_head(const uint4 (&ch)[NS], uint32_t s, uint32_t hl, uint32_t L, bool odd,
+                                                 bool present, uint32_t &ipv, uint32_t &l4f, uint32_t &hsum,
+                                                 uint32_t &seed, uint32_t &hdr)
+{
+    ipv = 0;
+    l4f = kNoField;
+    hsum = 0;
+    seed = 0;
+    hdr = 0;
+    if (!present)
+        return RNS_TX_MALFORMED;
+    uint32_t h[10];
+    head40(ch, s, h);
+    uint32_t field;
+    bool v4;
+    if (!tx_parse(h, L, hl, hdr, field, seed, v4))
+        return RNS_TX_MALFORMED;
+    const int lo = static_cast<int>(s);
+    uint8_t st = 0;
+    if (v4) {
+        const uint32_t H = stash_sum_le(ch, lo, lo + static_cast<int>(hdr)) - stash_sum_le(ch, lo + 10, lo + 12);
+        ipv = finalize_bits(H, odd, false, 0u, true, RNS_FLAG_COMPLEMENT);
+        st |= RNS_TX_IP_FILLED;
+    }
+    if (field != kNoField && L - hdr >= field + 2 && hdr + field + 2 <= hl) {
+        l4f = hdr + field;
+        const int f = lo + static_cast<int>(l4f);
+        hsum = stash_sum_le(ch, lo + static_cast<int>(hdr), lo + static_cast<int>(hl)) - stash_sum_le(ch, f, f + 2);
+        st |= RNS_TX_L4_FILLED;
+    }
+    return st;
+}
+
+// set_be16 of a finished field at absolute arena offset fp (util.rs:132-135); AUX = the buffer
+// store's cache-policy bits
+template <bool BUF, int AUX = 0>
 __device__ __forceinline__ void store_field(const CsumArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint64_t fp, uint32_t v)
 {
     uint8_t *w8 = const_cast<uint8_t *>(a.arena);
@@ -739,7 +803,7 @@ __device__ __forceinline__ void store_field(const CsumArgs &a, __amdgpu_buffer_r
         w8[fp + 1] = static_cast<uint8_t>(v);
     } else if constexpr (BUF) {
         __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(bswap16_u32(v & 0xffffu)), rsrc,
-                                              static_cast<uint32_t>(fp), 0, 0);
+                                              static_cast<uint32_t>(fp), 0, AUX);
     } else {
         *reinterpret_cast<uint16_t *>(w8 + fp) = static_cast<uint16_t>(bswap16_u32(v & 0xffffu));
     }
@@ -885,15 +949,27 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : RNS_ROWS_TX_OCC) void csum_rows_t
 // field) and whose payloads ascend at 16-byte starts with bounded gaps takes the rows; any
 // other wave takes an exact per-packet loop (the whole wave sums one fragment at a time,
 // big-endian words mod 2^32: util.rs:88-106 literally), so the hint never changes a result.
+//
+// FIN (rns_tx_fill_chain_dev): the whole transmit finalize of such chains — the head fragment
+// holds the IP header and the L4 header behind it (alloc_header prepends both into one fragment,
+// buf.rs:262-291), so the owner parses its head (chain_tx_head), forms the pseudo-header from the
+// head's addresses and the chain's length, sums the head's L4 part, and stores the L4 field and
+// the IPv4 header checksum into the head: tcp.rs:957-973, udp.rs:151-171, icmp.rs:87-112,
+// ip.rs:140-160 over [head[hdr..], payload...] exactly as compute_buffer_ones_comp folds it.
+// Heads of up to 80 bytes from their 16-byte boundary (an IPv6 + TCP head at any start) take
+// the rows; the status byte goes to a.status.
 // ---------------------------------------------------------------------------
 #ifndef RNS_TXROWS_OCC  // waves/SIMD bound of the transmit-rows kernel
 #define RNS_TXROWS_OCC 5  // (zero scratch at 86-89 VGPRs; 6 spills 32-116 B/lane)
 #endif
-constexpr uint32_t kTxHeadMax = 64;  // (head start & 15) + head length: at most 4 chunks
+constexpr uint32_t kTxHeadMax = 64;  // (head start & 15) + head length: at most 4 chunks (5 for FIN)
 
-template <bool NT, bool BUF, int D, bool FILL>
+template <bool NT, bool BUF, int D, bool FILL, bool FIN = false>
 __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const CsumArgs a)
 {
+    static_assert(!(FILL && FIN), "FIN finds its fields itself");
+    constexpr uint32_t kNH = FIN ? 5u : 4u;  // head chunks the fast path holds
+    constexpr uint32_t kHeadMax = 16u * kNH;
     const uint32_t lane = threadIdx.x;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.arena), static_cast<short>(0), static_cast<int>(BUF ? buf_records(a) : 0), 0x00020000);
@@ -941,10 +1017,12 @@ __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const C
     bool bad = live && (!rng_ok || (nfr <= kF && !all_in));
     if constexpr (FILL)
         bad = bad || (live && (nfr == 0 || !(fo <= hl && hl - fo >= 2u)));
+    if constexpr (FIN)
+        bad = bad || (live && nfr == 0);
     const bool has_pay = live && !bad && plen != 0;
     const uint64_t po = o[1];
     const bool shape = !live || bad ||
-                       (run && plen <= 0xFFFFu && (o[0] & 15u) + hl <= kTxHeadMax && (!has_pay || (po & 15u) == 0));
+                       (run && plen <= 0xFFFFu && (o[0] & 15u) + hl <= kHeadMax && (!has_pay || (po & 15u) == 0));
     // the wave's payload region: ascending, 16-byte starts, gaps bounded (else the exact loop)
     const uint64_t pm = __ballot(has_pay);
     uint64_t r0 = 0;
@@ -971,17 +1049,22 @@ __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const C
     }
     const bool fast = !__ballot(!shape) && region;
     uint32_t res = 0;  // the folded sum (before the complement)
+    uint32_t fst = RNS_TX_MALFORMED, ipv = 0, l4f = kNoField;  // FIN: status, IPv4 checksum, L4 field
     if (fast) {
         // the owner's head: its chunks issued before the rows, consumed after the first group
         const uint64_t hb = o[0] & ~15ull;
         const uint32_t hs = static_cast<uint32_t>(o[0] & 15u), span = live && !bad ? hs + hl : 0u;
-        uint4 h[4];
+        uint4 h[kNH];
 #pragma unroll
-        for (uint32_t i = 0; i < 4; ++i)
+        for (uint32_t i = 0; i < kNH; ++i)
             h[i] = own_chunk<BUF>(a, rsrc, recs, hb, span, i);
         uint32_t acc1 = 0;
         auto head = [&]() {
-            uint32_t hsum = 0;
+            uint32_t hsum = 0, sd = seed;
+            if constexpr (FIN) {
+                uint32_t hd;
+                fst = chain_tx_head<kNH>(h, hs, hl, hl + plen, (o[0] & 1u) != 0, live && !bad, ipv, l4f, hsum, sd, hd);
+            } else {
 #pragma unroll
             for (uint32_t i = 0; i < 4; ++i) {
                 const int lo = static_cast<int>(hs) - 16 * static_cast<int>(i), hi = static_cast<int>(span) - 16 * static_cast<int>(i);
@@ -989,6 +1072,7 @@ __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const C
                 hsum = __builtin_amdgcn_sad_u16(keep_bytes(h[i].y, lo, hi, 4), 0, hsum);
                 hsum = __builtin_amdgcn_sad_u16(keep_bytes(h[i].z, lo, hi, 8), 0, hsum);
                 hsum = __builtin_amdgcn_sad_u16(keep_bytes(h[i].w, lo, hi, 12), 0, hsum);
+            }
             }
             if constexpr (FILL) {  // the field counts as zero (buf.rs:286-288)
                 const uint32_t w[16] = {h[0].x, h[0].y, h[0].z, h[0].w, h[1].x, h[1].y, h[1].z, h[1].w,
@@ -1005,7 +1089,7 @@ __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const C
             }
             const uint32_t x = fold16(hsum);
             const uint32_t g = (o[0] & 1u) ? x : bswap16_u32(x);
-            const uint32_t t = seed + g;  // util.rs:89-103 with in_checksum = seed (no wrap: <= 0x1fffe)
+            const uint32_t t = sd + g;  // util.rs:89-103 with in_checksum = seed (no wrap: <= 0x1fffe)
             acc1 = (t & 0xffff) + (t >> 16);
         };
         uint32_t mine = 0;
@@ -1019,34 +1103,64 @@ __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const C
         res = has_pay ? (t & 0xffff) + (t >> 16) : acc1;
     } else {
         // ---- the exact per-packet loop: the whole wave sums one fragment at a time ----
-        uint64_t todo = __ballot(live && rng_ok && nfr != 0 && !bad);
+        uint32_t sd = seed, hd = 0;
+        if constexpr (FIN) {
+            // the chain's length, and every fragment (not just the first kF) inside the arena
+            uint32_t lt = 0;
+            bool in = true;
+            if (live && rng_ok) {
+                for (uint32_t f = f0; f < f1; ++f) {
+                    const uint64_t so = a.off[f] + a.base_adjust;
+                    const uint32_t lf = a.len[f];
+                    in = in && so <= a.arena_bytes && lf <= a.arena_bytes - so;
+                    lt += lf;
+                }
+            }
+            bad = bad || (live && !in);
+            // the head's first 81-96 bytes from its 16-byte boundary: the IP header and the L4 field
+            const uint64_t hb = o[0] & ~15ull;
+            const uint32_t s0 = static_cast<uint32_t>(o[0] & 15u);
+            uint4 own[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+                own[i] = own_chunk<BUF>(a, rsrc, recs, hb, live && !bad ? s0 + hl : 0u, i);
+            uint32_t hsum;
+            fst = chain_tx_head<6>(own, s0, hl, lt, (o[0] & 1u) != 0, live && !bad, ipv, l4f, hsum, sd, hd);
+        }
+        uint64_t todo = FIN ? __ballot(live && !bad && l4f != kNoField) : __ballot(live && rng_ok && nfr != 0 && !bad);
         bool lbad = bad;
-        res = seed;  // (a packet without fragments)
+        res = sd;  // (a packet without fragments)
         while (todo) {
             const uint32_t ow = static_cast<uint32_t>(__builtin_ctzll(todo));
             todo &= todo - 1;
             const uint32_t F0 = __builtin_amdgcn_readlane(f0, ow), F1 = __builtin_amdgcn_readlane(f1, ow);
-            const uint32_t FO = __builtin_amdgcn_readlane(fo, ow);
-            uint32_t acc = __builtin_amdgcn_readlane(seed, ow);
+            // FIN: the L4 part of the head starts HD bytes in, its field FO bytes after that
+            const uint32_t HD = FIN ? __builtin_amdgcn_readlane(hd, ow) : 0u;
+            const uint32_t FO = FIN ? __builtin_amdgcn_readlane(l4f, ow) - HD : __builtin_amdgcn_readlane(fo, ow);
+            uint32_t acc = __builtin_amdgcn_readlane(sd, ow);
             bool pbad = false;
             for (uint32_t f = F0; f < F1; ++f) {
-                const uint64_t st = a.off[f] + a.base_adjust;
-                const uint32_t L = a.len[f];
+                uint64_t st = a.off[f] + a.base_adjust;
+                uint32_t L = a.len[f];
                 if (!(st <= a.arena_bytes && L <= a.arena_bytes - st)) {
                     pbad = true;
                     break;
+                }
+                if (FIN && f == F0) {  // the IP header was prepended after the L4 checksum
+                    st += HD;
+                    L -= HD;
                 }
                 if (L == 0)  // an empty fragment adds nothing (the reference panics on it)
                     continue;
                 const Pkt k = make_pkt(st, L);
                 const uint32_t w_hi = (st & 1) ? 0x01000100u : 0x00010001u;
-                const uint64_t fpos = st + FO;  // FILL: the field in the head fragment (f == F0)
+                const uint64_t fpos = st + FO;  // FILL / FIN: the field in the head fragment (f == F0)
                 uint32_t hsb = 0, lsb = 0;
                 for (uint32_t cc = 0; cc < k.nch; cc += 64) {
                     uint4 w[1];
                     issue_pass<64, 1, NT, BUF, 1>(a, rsrc, k, cc + lane, w);
                     mask_edges<64, 1, 1>(k, cc + lane, w);
-                    if (FILL && f == F0) {
+                    if ((FILL || FIN) && f == F0) {
                         const uint64_t cs = (st & ~15ull) + (static_cast<uint64_t>(cc + lane) << 4);
                         const int lo = static_cast<int>(static_cast<int64_t>(fpos) - static_cast<int64_t>(cs));
                         if (lo > -2 && lo < 16) {  // zero the field's bytes in this chunk
@@ -1072,7 +1186,15 @@ __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const C
         bad = lbad;
     }
     const bool okp = live && !bad;
-    const uint32_t r = (a.flags & RNS_FLAG_COMPLEMENT) ? res ^ 0xffffu : res;
+    const uint32_t r = (FIN || (a.flags & RNS_FLAG_COMPLEMENT)) ? res ^ 0xffffu : res;
+    if constexpr (FIN) {  // set_be16 into header_mut(): the L4 field, then ip.rs:158-159's
+        if (okp && (fst & RNS_TX_L4_FILLED))
+            store_field<BUF, RNS_STREAM_OUT_AUX>(a, rsrc, o[0] + l4f, r);
+        if (okp && (fst & RNS_TX_IP_FILLED))
+            store_field<BUF, RNS_STREAM_OUT_AUX>(a, rsrc, o[0] + 10, ipv);
+        if (live && a.status)
+            a.status[p] = okp ? static_cast<uint8_t>(fst) : static_cast<uint8_t>(RNS_TX_MALFORMED);
+    }
     // (field stores as buffer stores with the result stores' sc0|sc1 bits: IMIX 604.4 -> 598.4 us,
     // c3 251.0 -> 245.7 against ordinary stores; nontemporal 595.8 / 246.4: session r05e)
     if constexpr (FILL) {

@@ -82,6 +82,7 @@ template <bool FILL>
 int launch_txrows(const CsumArgs &a, hipStream_t st);
 extern template int launch_txrows<false>(const CsumArgs &, hipStream_t);
 extern template int launch_txrows<true>(const CsumArgs &, hipStream_t);
+int launch_txfin(const CsumArgs &a, hipStream_t st);
 // k_stash.hip: the class kernel's stash modes on one-wave workgroups
 int launch_fill(const CsumArgs &a, dim3 grid, hipStream_t st);
 int launch_rx(const CsumArgs &a, dim3 grid, hipStream_t st);

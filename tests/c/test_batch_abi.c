@@ -632,6 +632,102 @@ static int test_tx_rx_packed(hipStream_t st)
     return 0;
 }
 
+/* Transmit finalize of NetBuffer chains (rns_tx_fill_chain_dev): heads holding the IPv4 header
+ * and the L4 header (TCP 20 B, UDP 8 B, ICMP 9 B: an odd head part) back to back from an odd
+ * offset, payloads as 512-byte NetBuffer fragments packed at 16-byte starts.  Expected: the IPv4
+ * header checksum (ip.rs:158-159) and the L4 checksum folded per fragment over [L4 header,
+ * payload fragments] (util.rs:112-119 as tcp.rs:957-973 / udp.rs:158-171 / icmp.rs:91-94 call
+ * it) with the fields zeroed; every other byte unchanged. */
+static int test_tx_chain(hipStream_t st)
+{
+    const uint32_t n = 2000;
+    const uint8_t src[4] = {10, 0, 0, 1}, dst[4] = {10, 0, 0, 2};
+    uint32_t *first = malloc((n + 1) * sizeof *first), *hl = malloc(n * sizeof *hl), *pl = malloc(n * sizeof *pl);
+    uint8_t *proto = malloc(n), *status = malloc(n);
+    uint32_t nf = 0;
+    uint64_t hpos = 3, ppos = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t r = next_u64();
+        proto[i] = (i % 3 == 0) ? 6 : (i % 3 == 1) ? 17 : 1;
+        hl[i] = 20u + (proto[i] == 6 ? 20u : proto[i] == 17 ? 8u : 9u);
+        pl[i] = (uint32_t)((r >> 8) % 1461u);
+        nf += 1u + (pl[i] + 511u) / 512u;
+        hpos += hl[i];
+    }
+    uint64_t *off = malloc(nf * sizeof *off);
+    uint32_t *len = malloc(nf * sizeof *len);
+    ppos = (hpos + 4095) & ~4095ull;
+    hpos = 3;
+    nf = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        first[i] = nf;
+        off[nf] = hpos;
+        len[nf++] = hl[i];
+        hpos += hl[i];
+        for (uint32_t k = 0; k * 512u < pl[i]; ++k) {
+            off[nf] = ppos + 512u * k;
+            len[nf++] = pl[i] - 512u * k < 512u ? pl[i] - 512u * k : 512u;
+        }
+        ppos = (ppos + pl[i] + 15) & ~15ull;
+    }
+    first[n] = nf;
+    const uint64_t bytes = ppos + 16;
+    uint8_t *arena = malloc(bytes), *ref = malloc(bytes), *back = malloc(bytes);
+    fill_random(arena, bytes);
+    for (uint32_t i = 0; i < n; ++i) {
+        uint8_t *h = arena + off[first[i]];
+        const uint32_t tot = hl[i] + pl[i];
+        h[0] = 0x45; h[1] = 0; h[2] = (uint8_t)(tot >> 8); h[3] = (uint8_t)tot;
+        h[6] = 0x40; h[7] = 0; h[8] = 64; h[9] = proto[i];
+        memcpy(h + 12, src, 4);
+        memcpy(h + 16, dst, 4);                      /* both checksum fields keep their garbage */
+    }
+    memcpy(ref, arena, bytes);
+    for (uint32_t i = 0; i < n; ++i) {
+        uint8_t *h = ref + off[first[i]], *seg = h + 20;
+        const uint32_t field = proto[i] == 6 ? 16u : proto[i] == 17 ? 6u : 2u;
+        h[10] = h[11] = 0;
+        const uint32_t ipc = (uint32_t)oracle_compute_checksum(h, 20);
+        h[10] = (uint8_t)(ipc >> 8); h[11] = (uint8_t)ipc;
+        seg[field] = seg[field + 1] = 0;
+        int32_t acc = proto[i] == 1 ? 0 : oracle_compute_pseudo_header_checksum(src, 4, dst, 4, hl[i] - 20u + pl[i], proto[i]);
+        acc = oracle_compute_ones_comp((uint16_t)acc, seg, hl[i] - 20u);
+        for (uint32_t f = first[i] + 1; f < first[i + 1]; ++f)
+            acc = oracle_compute_ones_comp((uint16_t)acc, ref + off[f], len[f]);
+        const uint32_t l4 = 0xffffu ^ (uint32_t)acc;
+        seg[field] = (uint8_t)(l4 >> 8); seg[field + 1] = (uint8_t)l4;
+    }
+    uint8_t *d_arena, *d_status;
+    uint64_t *d_off;
+    uint32_t *d_len, *d_first;
+    HIP_OK(hipMalloc((void **)&d_arena, bytes));
+    HIP_OK(hipMalloc((void **)&d_off, nf * sizeof *off));
+    HIP_OK(hipMalloc((void **)&d_len, nf * sizeof *len));
+    HIP_OK(hipMalloc((void **)&d_first, (n + 1) * sizeof *first));
+    HIP_OK(hipMalloc((void **)&d_status, n));
+    HIP_OK(hipMemcpy(d_arena, arena, bytes, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_off, off, nf * sizeof *off, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_len, len, nf * sizeof *len, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_first, first, (n + 1) * sizeof *first, hipMemcpyHostToDevice));
+    CHECK(rns_tx_fill_chain_dev(d_arena, bytes, d_off, d_len, nf, d_first, n, d_status, st) == RNS_OK,
+          "rns_tx_fill_chain_dev");
+    HIP_OK(hipStreamSynchronize(st));
+    HIP_OK(hipMemcpy(back, d_arena, bytes, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(status, d_status, n, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n; ++i)
+        CHECK(status[i] == (RNS_TX_IP_FILLED | RNS_TX_L4_FILLED), "chain tx status %u: %02x", i, status[i]);
+    uint64_t diff = 0;
+    for (uint64_t b = 0; b < bytes; ++b)
+        diff += back[b] != ref[b];
+    CHECK(diff == 0, "chain tx: %llu arena bytes differ from the oracle's", (unsigned long long)diff);
+    CHECK(rns_tx_fill_chain_dev(d_arena, bytes, d_off, d_len, nf, NULL, n, d_status, st) == RNS_E_INVALID,
+          "NULL first");
+    hipFree(d_arena); hipFree(d_off); hipFree(d_len); hipFree(d_first); hipFree(d_status);
+    free(first); free(hl); free(pl); free(proto); free(status); free(off); free(len); free(arena); free(ref);
+    free(back);
+    return 0;
+}
+
 int main(void)
 {
     const uint32_t n = 40000;
@@ -731,7 +827,7 @@ int main(void)
     /* 2b. the packed entry bench.py times, the fragment-chain entry, transmit finalize and
      *     receive verify: each against the oracle's util.rs restatement */
     if (test_packed(st) || test_strided(st) || test_chains(st) || test_chain_fill(st) || test_chain_fill_txpacked(st) || test_tx_rx(st) ||
-        test_tx_rx_packed(st))
+        test_tx_rx_packed(st) || test_tx_chain(st))
         return 2;
 
     /* 3. errors come back as status codes, never as aborts */

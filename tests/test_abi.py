@@ -70,6 +70,7 @@ def test_batch_calls_fail_loudly_without_gpu():
     assert lib.rns_tx_fill_packed_dev(fake, 64, fake, fake, 4, 1, None, 0, None) == _lib.RNS_E_NODEVICE
     assert lib.rns_rx_verify_strided_dev(fake, 64, 0, 64, fake, 1, fake, fake, fake, None,
                                          None) == _lib.RNS_E_NODEVICE
+    assert lib.rns_tx_fill_chain_dev(fake, 64, fake, fake, 1, fake, 1, None, None) == _lib.RNS_E_NODEVICE
 
 
 def test_argument_errors_before_the_device():
@@ -87,6 +88,9 @@ def test_argument_errors_before_the_device():
     assert lib.rns_rx_verify_strided_dev(fake, 64, 0, big, fake, 3, fake, fake, fake, None,
                                          None) == _lib.RNS_E_INVALID
     assert lib.rns_tx_fill_packed_dev(fake, 64, fake, fake, 3, 1, None, 0, None) == _lib.RNS_E_INVALID
+    assert lib.rns_tx_fill_chain_dev(fake, 64, fake, fake, 1, None, 1, None, None) == _lib.RNS_E_INVALID
+    assert lib.rns_tx_fill_chain_dev(fake, 64, fake, fake, 1, fake, _lib.RNS_CHAIN_MAX_PACKETS + 1, None,
+                                     None) == _lib.RNS_E_INVALID
     end = ctypes.c_uint64()
     assert lib.rns_io_recv_batch_packed(0, fake, 4096, 70000, 4, fake, fake, ctypes.byref(end), 0) == \
         _lib.RNS_E_INVALID

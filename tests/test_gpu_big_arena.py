@@ -10,7 +10,7 @@ translated), and for the in-place fills every byte of every window is compared.
 Entries covered: the packed checksum (rows kernel D = 8 and D = 16, the tiny rounds
 kernel, the unaligned-packing class kernel, a first block at an odd offset), the strided
 form, the packed and explicit transmit fills, packed, explicit and strided receive verify, the
-explicit and packed transmit finalize, fragment chains (nontemporal and temporal class passes, each through a
+explicit, packed and chain transmit finalize, fragment chains (nontemporal and temporal class passes, each through a
 buffer window based at its pass's fragments and through 64-bit loads for passes spanning more
 than 4 GiB; the runs hint, which is ignored past 4 GiB) and the head-fragment chain fill.  Reference: util.rs:88-119,
 tcp.rs:838-850 / 957-973, udp.rs:158-171, icmp.rs:46-112, ip.rs:76-80 / 158-159.
@@ -23,7 +23,8 @@ from oracle import oracle as O
 from rustnetworkstack_amd import _lib
 from rustnetworkstack_amd.batch import (csum_batch_packed, csum_batch_strided, csum_chain, csum_chain_fill,
                                         csum_fill, csum_fill_packed, fill_splitmix64, packed_layout, rx_verify,
-                                        rx_verify_packed, rx_verify_strided, tx_fill, tx_fill_packed)
+                                        rx_verify_packed, rx_verify_strided, tx_fill, tx_fill_chain,
+                                        tx_fill_packed)
 from test_gpu_rx import make_packets
 from test_gpu_tx import outgoing
 from test_rx_oracle import L4, L6, ipv4, tcp_seg, R4
@@ -356,6 +357,45 @@ def test_packed_transmit_finalize(oracle, win, hint):
         want = np.concatenate(host)
         diff = np.flatnonzero(got != want)
         assert diff.size == 0, [(int(d), int(got[d]), int(want[d])) for d in diff[:8]]
+    finally:
+        win.restore()
+
+
+@pytest.mark.parametrize("shape", ["tx", "any"])
+def test_chain_transmit_finalize(oracle, win, shape):
+    """rns_tx_fill_chain_dev's BUF=false instantiation: every kind of outgoing datagram as a
+    [head, payload pieces] chain in each window (the middle layout across the 4 GiB line), in
+    the transmit shape (the rows) and scattered (the exact loop); every window byte and status
+    against oracle.tx_chain_fill_ref."""
+    from test_gpu_tx_chain import expected, layout
+    inp = [h.copy() for h in win.orig]
+    want = [h.copy() for h in win.orig]
+    offs, lns, firsts, want_st = [], [], [np.zeros(1, np.uint32)], []
+    nf = 0
+    for k in range(3):
+        pk = outgoing(600 + (5 if k == 2 else 0), 0x7D0 + k)
+        arena, heads, hoffs, placed, off, ln, first = layout(pk, 0x7D8 + k, shape=shape)
+        w_arena, st = expected(oracle, arena, heads, hoffs, placed)
+        size = arena.size
+        assert size <= SPAN
+        rel = (0, (SPAN // 2 - size // 2) & ~15, (SPAN - size) & ~15)[k]
+        inp[k][rel:rel + size] = arena
+        want[k][rel:rel + size] = w_arena
+        offs.append(off + np.uint64(win.starts[k] + rel))
+        lns.append(ln)
+        firsts.append(first[1:] + np.uint32(nf))
+        nf += off.size
+        want_st.append(st)
+    try:
+        win.write(inp)
+        st = tx_fill_chain(win.arena, dev(np.concatenate(offs), np.int64), dev(np.concatenate(lns), np.int32),
+                           dev(np.concatenate(firsts), np.int32))
+        torch.cuda.synchronize()
+        assert np.array_equal(st.cpu().numpy(), np.concatenate(want_st))
+        got = np.concatenate(win.snapshot())
+        w = np.concatenate(want)
+        diff = np.flatnonzero(got != w)
+        assert diff.size == 0, [(int(d), int(got[d]), int(w[d])) for d in diff[:8]]
     finally:
         win.restore()
 

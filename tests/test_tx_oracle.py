@@ -74,3 +74,65 @@ def test_not_produced_by_the_stack_left_alone():
     tiny = zero(ipv4(6, b"x" * 17), 10)
     out, st = O.tx_fill_ref(tiny)
     assert st == O.TX_IP_FILLED                         # segment too short for [16..18]
+
+
+def chain(pkt, cuts):
+    """pkt cut at the given offsets: [pkt[:c0], pkt[c0:c1], ...]."""
+    b = [0] + list(cuts) + [len(pkt)]
+    return [pkt[b[i]:b[i + 1]] for i in range(len(b) - 1)]
+
+
+def test_chain_fill_equals_whole_datagram_fill_for_even_pieces():
+    """A head holding the IP and L4 headers, then payload pieces of even length (the
+    reference's 512-byte NetBuffer fragments): the same bytes tx_fill_ref stores in the
+    contiguous datagram, in the head, and the same status."""
+    cases = [
+        (ipv4(6, tcp_seg(L4, R4, b"p" * 1460)), 40),
+        (ipv6(6, tcp_seg(L6, R6, b"q" * 1000)), 60),
+        (ipv4(17, tcp_seg(L4, R4, b"r" * 777, proto=17, field=6, hlen=8)), 28),
+        (ipv4(1, icmp4(b"s" * 600)), 28),
+        (ipv6(58, tcp_seg(L6, R6, b"t" * 333, proto=58, field=2, hlen=4)), 48),
+        (ipv4(6, tcp_seg(L4, R4, b"u" * 100), ihl=15), 80),
+    ]
+    for pkt, hl in cases:
+        pkt = zero(pkt, 10) if pkt[0] >> 4 == 4 else pkt
+        want, st = O.tx_fill_ref(pkt)
+        for step in (512, 2, 1000):
+            cuts = list(range(hl, len(pkt), step))
+            frags = chain(pkt, cuts)
+            head, st2 = O.tx_chain_fill_ref(frags)
+            assert st2 == st and head == want[:hl]
+        # the whole datagram as one head fragment
+        assert O.tx_chain_fill_ref([pkt]) == (want, st)
+
+
+def test_chain_fill_folds_odd_pieces_per_fragment():
+    """An odd-length L4 header part or payload piece pairs its bytes from its own start
+    (util.rs:112-119 folds every fragment on its own): the L4 value is the per-fragment fold,
+    not the contiguous sum."""
+    pkt = ipv4(6, tcp_seg(L4, R4, bytes(range(1, 200))))
+    frags = chain(pkt, [41, 100, 151])                     # head with 21 L4 bytes, odd pieces
+    head, st = O.tx_chain_fill_ref(frags)
+    assert st == O.TX_IP_FILLED | O.TX_L4_FILLED
+    l4 = bytearray(frags[0][20:])
+    l4[16:18] = b"\x00\x00"
+    ph = O.pseudo_header_py(pkt[12:16], pkt[16:20], len(pkt) - 20, 6)
+    want = O.buffer_ones_comp_py(ph, [bytes(l4)] + frags[1:]) ^ 0xFFFF
+    assert int.from_bytes(head[36:38], "big") == want
+    assert want != int.from_bytes(O.tx_fill_ref(pkt)[0][36:38], "big")
+    assert O.checksum_py(head[:20]) == 0                  # the IP header verifies
+
+
+def test_chain_fill_rejects_and_partial_fills():
+    pkt = ipv4(6, tcp_seg(L4, R4, b"x" * 64))
+    assert O.tx_chain_fill_ref([]) == (b"", O.TX_MALFORMED)
+    assert O.tx_chain_fill_ref([b"", pkt]) == (b"", O.TX_MALFORMED)
+    assert O.tx_chain_fill_ref([pkt[:19], pkt[19:]]) == (pkt[:19], O.TX_MALFORMED)   # IP header split
+    v6 = ipv6(6, tcp_seg(L6, R6, b"y" * 10))
+    assert O.tx_chain_fill_ref([v6[:39], v6[39:]])[1] == O.TX_MALFORMED
+    head, st = O.tx_chain_fill_ref([pkt[:30], pkt[30:]])                               # field past the head
+    assert st == O.TX_IP_FILLED and head[20:30] == pkt[20:30] and O.checksum_py(head[:20]) == 0
+    head, st = O.tx_chain_fill_ref([v6[:40], v6[40:]])                                 # IPv6: no IP field
+    assert st == 0 and head == v6[:40]
+    head, st = O.tx_chain_fill_ref([pkt[:38], b"", pkt[38:]])                          # empty piece: nothing
+    assert st == O.TX_IP_FILLED | O.TX_L4_FILLED and head == O.tx_fill_ref(pkt)[0][:38]

@@ -16,6 +16,9 @@ batch checksum, on the headline batch (2^20 x 1500 B) and on IMIX:
              20-byte TCP head fragments back to back in a header region, the payload as one
              fragment or as 512-byte NetBuffer fragments), next to the plain chain checksum
              of the same chains (chain_tx)
+* tx_chain — rns_tx_fill_chain_dev: whole-datagram finalize of the same transmit shape with
+             40-byte IPv4 + TCP head fragments (the layout alloc_header builds, buf.rs:262-291),
+             payload as one fragment or 512-byte NetBuffer fragments (round 6)
 
 Timing: one pair of HIP events around K back-to-back launches on the launch stream,
 median of R rounds.  GB/s counts algorithmic bytes (payload read + result bytes
@@ -118,6 +121,9 @@ def main():
         if "chain_fill" in ops:
             for frag in (int(x) for x in args.tx_frags.split(",")):
                 r.update(bench_chain_fill(cfg, dev, args, frag))
+        if "tx_chain" in ops:
+            for frag in (int(x) for x in args.tx_frags.split(",")):
+                r.update(bench_tx_chain(cfg, dev, args, frag))
         if "fill" in ops:
             ms = timed(lambda: csum_fill(b.arena, b.off, b.length, b.seed, field_off=16), args.steps, args.rounds)
             r["fill"] = {"us": round(ms * 1e3, 1), "GBps": round((pay + 2 * n) / ms / 1e6, 1)}
@@ -237,6 +243,35 @@ def bench_chain_fill(cfg, dev, args, frag):
     del arena
     torch.cuda.empty_cache()
     return res
+
+
+def bench_tx_chain(cfg, dev, args, frag):
+    """Whole-datagram transmit finalize over NetBuffer chains: 40-byte IPv4 + TCP heads back to
+    back in a header region, payloads packed at 16-byte starts (one fragment, or 512-byte ones)."""
+    from rustnetworkstack_amd.batch import fill_splitmix64, tx_fill_chain
+    from rustnetworkstack_amd.workloads import tx_chain_layout
+    t = tx_chain_layout(cfg, head=40, frag=frag)
+    n, pay, nf = t.n, t.payload_bytes, int(t.frag_off.shape[0])
+    arena = torch.empty(t.arena_bytes + 64, dtype=torch.uint8, device=dev)
+    fill_splitmix64(arena, t.data_seed)
+    hoff = torch.from_numpy(t.frag_off[t.first[:-1].astype(np.int64)].view(np.int64)).to(dev)
+    hdr = np.frombuffer(bytes.fromhex("4500000000004000400600000000000000000000"), dtype=np.uint8).copy()
+    hdr[12:16] = [192, 168, 1, 1]
+    hdr[16:20] = np.frombuffer(L4, dtype=np.uint8)
+    idx = hoff.view(-1, 1) + torch.arange(20, device=dev)
+    arena[idx.flatten()] = torch.from_numpy(hdr).to(dev).repeat(n)
+    del idx
+    d_fo = torch.from_numpy(t.frag_off.view(np.int64)).to(dev)
+    d_fl = torch.from_numpy(t.frag_len.view(np.int32)).to(dev)
+    d_first = torch.from_numpy(t.first.view(np.int32)).to(dev)
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    ms = timed(lambda: tx_fill_chain(arena, d_fo, d_fl, d_first, status=st), args.steps, args.rounds)
+    filled = int((st == 3).sum().item())
+    tag = "tx_chain" if frag == 0 else f"tx_chain{frag}"
+    del arena
+    torch.cuda.empty_cache()
+    return {tag: {"us": round(ms * 1e3, 1), "GBps": round((pay + n) / ms / 1e6, 1), "filled": filled,
+                  "packets": n, "fragments": nf}}
 
 
 def bench_chain_netbuf(lay, dev, args, shuffled=False, runs=False):
