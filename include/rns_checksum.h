@@ -408,6 +408,17 @@ int rns_csum_batch_multi_dev(const rns_dev_batch *batches, uint32_t nbatches, ui
 int rns_io_recv_batch(int fd, uint8_t *h_arena, uint64_t slot_bytes, uint32_t max_pkts, uint64_t *h_off,
                       uint32_t *h_len, int timeout_ms);
 int rns_io_send_batch(int fd, const uint8_t *h_arena, const uint64_t *h_off, const uint32_t *h_len, uint32_t n);
+/* Batched send_packet of NetBuffer chains (netif.rs:85-98: to_iovec over the fragments, then
+ * tun_send's writev, tun.c:88-90): datagram i = fragments [h_first[i], h_first[i+1]) of
+ * (h_frag_off, h_frag_len), at least one and at most RNS_IO_MAX_FRAGS of them (the reference's
+ * MAX_VECS, netif.rs:22), sent as ONE datagram gathered from its fragments — sendmmsg with one message per
+ * datagram on a socket fd, one writev per datagram on a TUN fd.  The chains of
+ * rns_tx_fill_chain_dev go out as they are (heads in a header region, payloads elsewhere).
+ * Returns the datagrams sent; a malformed range or too many fragments is RNS_E_INVALID before
+ * anything is sent. */
+#define RNS_IO_MAX_FRAGS 8u
+int rns_io_send_batch_chain(int fd, const uint8_t *h_arena, const uint64_t *h_frag_off, const uint32_t *h_frag_len,
+                            const uint32_t *h_first, uint32_t n_pkts);
 
 /* Batched receive straight into a PACKED arena (the descriptor form of
  * rns_rx_verify_packed_dev): every queued datagram (after waiting up to timeout_ms for the

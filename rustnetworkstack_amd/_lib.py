@@ -27,6 +27,7 @@ RNS_FLAG_COMPLEMENT = 0x1
 RNS_FLAG_CHAIN_RUNS = 0x2
 RNS_FLAG_CHAIN_TX_PACKED = 0x4
 RNS_CHAIN_MAX_PACKETS = 0xFFFFFFFF - 512  # packets per chain call (rns_checksum.h)
+RNS_IO_MAX_FRAGS = 8  # fragments per datagram of rns_io_send_batch_chain (netif.rs:22 MAX_VECS)
 RNS_RX_IP_OK = 0x01
 RNS_RX_L4_OK = 0x02
 RNS_RX_L4_UNCHECKED = 0x04
@@ -70,6 +71,7 @@ EXPORTED_SYMBOLS = (
     "rns_csum_batch_multi_dev",
     "rns_io_recv_batch",
     "rns_io_send_batch",
+    "rns_io_send_batch_chain",
     "rns_io_recv_batch_packed",
     "rns_host_alloc",
     "rns_host_free",
@@ -148,6 +150,7 @@ _SIGNATURES = {
     "rns_csum_batch_multi_dev": (_int, [ctypes.POINTER(RnsDevBatch), _u32, _u32]),
     "rns_io_recv_batch": (_int, [_int, _vp, _u64, _u32, _vp, _vp, _int]),
     "rns_io_send_batch": (_int, [_int, _vp, _vp, _vp, _u32]),
+    "rns_io_send_batch_chain": (_int, [_int, _vp, _vp, _vp, _vp, _u32]),
     "rns_io_recv_batch_packed": (_int, [_int, _vp, _u64, _u32, _u32, _vp, _vp, ctypes.POINTER(_u64), _int]),
     "rns_host_alloc": (_int, [_u64, ctypes.POINTER(_vp)]),
     "rns_host_free": (_int, [_vp]),

@@ -716,6 +716,29 @@ def send_batch(fd: int, arena: np.ndarray, off: np.ndarray, length: np.ndarray) 
     return r
 
 
+def send_batch_chain(fd: int, arena: np.ndarray, frag_off: np.ndarray, frag_len: np.ndarray,
+                     first: np.ndarray) -> int:
+    """Send NetBuffer chains (rns_io_send_batch_chain; batched send_packet, netif.rs:85-98):
+    datagram i = fragments ``first[i] .. first[i+1]`` of ``arena`` gathered into one datagram,
+    as to_iovec + tun_send's writev do.  Returns the number of datagrams sent."""
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    frag_off = np.ascontiguousarray(frag_off, dtype=np.uint64)
+    frag_len = np.ascontiguousarray(frag_len, dtype=np.uint32)
+    first = np.ascontiguousarray(first, dtype=np.uint32)
+    n = first.shape[0] - 1
+    if n < 0 or frag_off.shape[0] != frag_len.shape[0]:
+        raise ValueError("first needs n+1 entries; frag_off and frag_len one per fragment")
+    if n and int(first[-1]) > frag_off.shape[0]:
+        raise ValueError("first points past the fragment arrays")
+    if frag_off.shape[0] and int((frag_off + frag_len.astype(np.uint64)).max()) > arena.shape[0]:
+        raise ValueError("a fragment lies outside the arena")
+    r = _lib.load().rns_io_send_batch_chain(int(fd), arena.ctypes.data, frag_off.ctypes.data, frag_len.ctypes.data,
+                                            first.ctypes.data, n)
+    if r < 0:
+        raise _lib.ChecksumError(r, "rns_io_send_batch_chain")
+    return r
+
+
 class PinnedBuffer:
     """Page-locked host memory (rns_host_alloc) viewed as a numpy uint8 array."""
 

@@ -7,6 +7,8 @@
 // one copy (rns_rx_verify_packed_dev / rns_rx_verify_dev / rns_tx_fill_packed_dev).
 // On a socket fd a batch takes recvmmsg / sendmmsg: up to kMmsg datagrams per system
 // call; a TUN fd moves one datagram per read / writev (its driver has no batched call).
+// rns_io_send_batch_chain sends NetBuffer chains as send_packet does — each datagram's
+// fragments as one gather write (to_iovec + tun_send's writev, netif.rs:51-63, 85-98).
 #include <cerrno>
 #include <climits>
 #include <cstdint>
@@ -22,6 +24,7 @@
 namespace {
 
 constexpr unsigned kMmsg = 64;  // datagrams per recvmmsg / sendmmsg call
+constexpr uint32_t kChainIov = RNS_IO_MAX_FRAGS;  // fragments per datagram (netif.rs:22 MAX_VECS)
 
 // Waits up to timeout_ms for the first datagram; 1 = readable, 0 = timeout, < 0 = error.
 int wait_first(int fd, int timeout_ms)
@@ -290,6 +293,67 @@ int rns_io_send_batch(int fd, const uint8_t *h_arena, const uint64_t *h_off, con
             return i ? static_cast<int>(i) : RNS_E_IO;
     }
     return static_cast<int>(n);
+}
+
+int rns_io_send_batch_chain(int fd, const uint8_t *h_arena, const uint64_t *h_frag_off, const uint32_t *h_frag_len,
+                            const uint32_t *h_first, uint32_t n_pkts)
+{
+    if (fd < 0 || (n_pkts && (!h_arena || !h_first)))
+        return RNS_E_INVALID;
+    if (n_pkts > static_cast<uint32_t>(INT_MAX))
+        n_pkts = static_cast<uint32_t>(INT_MAX);
+    // every datagram's fragment range first (1..kChainIov fragments; an empty datagram would read
+    // as end-of-stream on a SOCK_SEQPACKET peer): a malformed one sends nothing
+    for (uint32_t i = 0; i < n_pkts; ++i) {
+        const uint32_t f0 = h_first[i], f1 = h_first[i + 1];
+        if (f1 <= f0 || f1 - f0 > kChainIov || !h_frag_off || !h_frag_len)
+            return RNS_E_INVALID;
+    }
+    uint32_t i = 0;
+    bool sock = true;
+    while (sock && i < n_pkts) {  // sockets: sendmmsg, each message one datagram's fragments
+        const unsigned k = n_pkts - i < kMmsg ? n_pkts - i : kMmsg;
+        struct mmsghdr mh[kMmsg];
+        struct iovec iov[kMmsg * kChainIov];
+        std::memset(mh, 0, sizeof(mh));
+        for (unsigned j = 0; j < k; ++j) {
+            const uint32_t f0 = h_first[i + j], nf = h_first[i + j + 1] - f0;
+            struct iovec *v = iov + j * kChainIov;
+            for (uint32_t f = 0; f < nf; ++f) {
+                v[f].iov_base = const_cast<uint8_t *>(h_arena + h_frag_off[f0 + f]);
+                v[f].iov_len = h_frag_len[f0 + f];
+            }
+            mh[j].msg_hdr.msg_iov = v;
+            mh[j].msg_hdr.msg_iovlen = nf;
+        }
+        int w;
+        do {
+            w = sendmmsg(fd, mh, k, 0);
+        } while (w < 0 && errno == EINTR);
+        if (w < 0) {
+            if (errno == ENOTSOCK && i == 0) {
+                sock = false;
+                break;
+            }
+            return i ? static_cast<int>(i) : RNS_E_IO;
+        }
+        i += static_cast<uint32_t>(w);
+    }
+    for (; i < n_pkts; ++i) {  // a TUN fd: one writev per datagram over its fragments, like tun_send
+        const uint32_t f0 = h_first[i], nf = h_first[i + 1] - f0;
+        struct iovec v[kChainIov];
+        for (uint32_t f = 0; f < nf; ++f) {
+            v[f].iov_base = const_cast<uint8_t *>(h_arena + h_frag_off[f0 + f]);
+            v[f].iov_len = h_frag_len[f0 + f];
+        }
+        ssize_t w;
+        do {
+            w = writev(fd, v, static_cast<int>(nf));
+        } while (w < 0 && errno == EINTR);
+        if (w < 0)
+            return i ? static_cast<int>(i) : RNS_E_IO;
+    }
+    return static_cast<int>(n_pkts);
 }
 
 }  // extern "C"

@@ -963,6 +963,9 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : RNS_ROWS_TX_OCC) void csum_rows_t
 #define RNS_TXROWS_OCC 5  // (zero scratch at 86-89 VGPRs; 6 spills 32-116 B/lane)
 #endif
 constexpr uint32_t kTxHeadMax = 64;  // (head start & 15) + head length: at most 4 chunks (5 for FIN)
+#ifndef RNS_TXFIN_RUNWRITE  // FIN: write a wave's back-to-back heads back as whole chunks
+#define RNS_TXFIN_RUNWRITE 1  // (IMIX 652.1-652.2 -> 632.5 us, c3 257.3 -> 256.0 against two 2-byte
+#endif                        //  stores per head: session r06h, txops / txops_rw)
 
 template <bool NT, bool BUF, int D, bool FILL, bool FIN = false>
 __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const CsumArgs a)
@@ -1050,6 +1053,31 @@ __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const C
     const bool fast = !__ballot(!shape) && region;
     uint32_t res = 0;  // the folded sum (before the complement)
     uint32_t fst = RNS_TX_MALFORMED, ipv = 0, l4f = kNoField;  // FIN: status, IPv4 checksum, L4 field
+    // FIN run write-back (RNS_TXFIN_RUNWRITE): a fast wave whose heads lie back to back (one run)
+    // stages its raw head chunks in LDS, patches its fields there and writes the run's whole
+    // 16-byte chunks back (full 64-byte segments, about half the write requests of two field
+    // stores per head); fields in the run's partial edge chunks take the 2-byte stores.
+    constexpr bool kRunWrite = FIN && RNS_TXFIN_RUNWRITE != 0;
+    bool runw = false;
+    uint64_t b0 = 0, r1 = 0;  // the run's first chunk boundary, its end
+    if constexpr (kRunWrite) {
+        const uint64_t hend = o[0] + hl;
+        const uint64_t pe = (static_cast<uint64_t>(static_cast<uint32_t>(
+                                 __shfl(static_cast<int>(hend >> 32), static_cast<int>(lane) - 1, 64)))
+                             << 32) |
+                            static_cast<uint32_t>(__shfl(static_cast<int>(hend), static_cast<int>(lane) - 1, 64));
+        const bool contig = !live || (!bad && (lane == 0 || o[0] == pe));
+        runw = fast && !__ballot(!contig);
+        const uint32_t last = 63u - static_cast<uint32_t>(__builtin_clzll(__ballot(live)));
+        b0 = ((static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(o[0] >> 32))))
+               << 32) |
+              static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(o[0])))) &
+             ~15ull;
+        r1 = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(hend >> 32), last)))
+              << 32) |
+             static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(hend), last));
+    }
+    __shared__ uint4 run_lds[kRunWrite ? 64u * kNH + 1u : 1u];
     if (fast) {
         // the owner's head: its chunks issued before the rows, consumed after the first group
         const uint64_t hb = o[0] & ~15ull;
@@ -1064,6 +1092,15 @@ __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const C
             if constexpr (FIN) {
                 uint32_t hd;
                 fst = chain_tx_head<kNH>(h, hs, hl, hl + plen, (o[0] & 1u) != 0, live && !bad, ipv, l4f, hsum, sd, hd);
+                if constexpr (kRunWrite) {
+                    if (runw) {  // the raw chunks the head touches (neighbours' bytes in them are raw too)
+                        const uint32_t q = static_cast<uint32_t>((hb - b0) >> 4);
+#pragma unroll
+                        for (uint32_t i = 0; i < kNH; ++i)
+                            if (16u * i < span)
+                                run_lds[q + i] = h[i];
+                    }
+                }
             } else {
 #pragma unroll
             for (uint32_t i = 0; i < 4; ++i) {
@@ -1188,9 +1225,40 @@ __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const C
     const bool okp = live && !bad;
     const uint32_t r = (FIN || (a.flags & RNS_FLAG_COMPLEMENT)) ? res ^ 0xffffu : res;
     if constexpr (FIN) {  // set_be16 into header_mut(): the L4 field, then ip.rs:158-159's
-        if (okp && (fst & RNS_TX_L4_FILLED))
+        const bool s4 = okp && (fst & RNS_TX_L4_FILLED), s3 = okp && (fst & RNS_TX_IP_FILLED);
+        uint64_t c0w = 0, c1w = 0;  // the run's whole chunks [c0w, c1w) (run write-back)
+        if constexpr (kRunWrite) {
+            if (runw) {
+                uint8_t *l8 = reinterpret_cast<uint8_t *>(run_lds);
+                const uint64_t q = o[0] - b0;
+                if (s4) {
+                    l8[q + l4f] = static_cast<uint8_t>(r >> 8);
+                    l8[q + l4f + 1] = static_cast<uint8_t>(r);
+                }
+                if (s3) {
+                    l8[q + 10] = static_cast<uint8_t>(ipv >> 8);
+                    l8[q + 11] = static_cast<uint8_t>(ipv);
+                }
+                __syncthreads();
+                c0w = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(o[0] & 15u)) == 0 ? b0 : b0 + 16;
+                c1w = r1 & ~15ull;
+                uint8_t *w8 = const_cast<uint8_t *>(a.arena);
+                for (uint64_t c = c0w + 16u * lane; c < c1w; c += 1024u) {
+                    const uint4 v = run_lds[(c - b0) >> 4];
+                    if constexpr (BUF) {
+                        const u32x4 y = {v.x, v.y, v.z, v.w};
+                        __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, static_cast<uint32_t>(c), 0, RNS_STREAM_OUT_AUX);
+                    } else {
+                        *reinterpret_cast<uint4 *>(w8 + c) = v;
+                    }
+                }
+            }
+        }
+        // (with the run write-back, only the fields not wholly inside its chunks)
+        auto outside = [&](uint64_t fp) { return !runw || fp < c0w || fp + 2 > c1w; };
+        if (s4 && outside(o[0] + l4f))
             store_field<BUF, RNS_STREAM_OUT_AUX>(a, rsrc, o[0] + l4f, r);
-        if (okp && (fst & RNS_TX_IP_FILLED))
+        if (s3 && outside(o[0] + 10))
             store_field<BUF, RNS_STREAM_OUT_AUX>(a, rsrc, o[0] + 10, ipv);
         if (live && a.status)
             a.status[p] = okp ? static_cast<uint8_t>(fst) : static_cast<uint8_t>(RNS_TX_MALFORMED);

@@ -5,7 +5,11 @@ Receive (RxPipeline): datagram fd -> pinned host arena -> HBM -> fused receive v
 16-byte boundary, rns_io_recv_batch_packed), so the copy to the GPU carries their bytes
 only — not whole 2048-byte slots — and the verify is the rows receive kernel
 (rns_rx_verify_packed_dev); ``packed=False`` keeps MRU slots and rns_rx_verify_dev.  Transmit (TxPipeline): pinned slots -> HBM -> transmit
-finalize -> the changed header bytes back -> datagram fd.
+finalize -> the changed header bytes back -> datagram fd.  TxChainPipeline does the same for
+datagrams built as the reference builds them — NetBuffer chains of a head fragment (IP + L4
+headers) and a payload — with the heads in a header region and the payloads in a payload region:
+only used bytes cross PCIe to the GPU, only the header region comes back, and each datagram leaves
+gathered from its two fragments (rns_io_send_batch_chain, like send_packet's writev).
 
 The reference handles one packet per loop iteration on its receive thread
 (packet_receive_thread lib.rs:26-31 -> recv_packet netif.rs:65-83 -> ip_input
@@ -26,7 +30,8 @@ from typing import Iterator
 import numpy as np
 import torch
 
-from .batch import PinnedBuffer, recv_batch, recv_batch_packed, rx_verify, rx_verify_packed, send_batch, tx_fill
+from .batch import (PinnedBuffer, recv_batch, recv_batch_packed, rx_verify, rx_verify_packed, send_batch,
+                    send_batch_chain, tx_fill, tx_fill_chain)
 
 MRU = 2048  # netif.rs:66
 
@@ -298,6 +303,167 @@ class TxPipeline:
         if ln.shape[0] == 0:
             return np.empty(0, dtype=np.uint8)
         return self._finish(fd, s, ln)
+
+    def close(self):
+        for s in self._sets:
+            s.close()
+
+
+class _ChainSet:
+    """One buffer set of TxChainPipeline: a pinned arena [header region | payload region], its
+    chain descriptors and statuses, and their HBM twins (the same offsets on both sides)."""
+
+    def __init__(self, dev: torch.device, max_pkts: int, head_region: int, payload_bytes: int):
+        self.host = PinnedBuffer(head_region + payload_bytes)
+        self.h_off = PinnedBuffer(8 * 2 * max_pkts)
+        self.h_len = PinnedBuffer(4 * 2 * max_pkts)
+        self.h_first = PinnedBuffer(4 * (max_pkts + 1))
+        self.h_status = PinnedBuffer(max_pkts)
+        self.d_arena = torch.empty(head_region + payload_bytes, dtype=torch.uint8, device=dev)
+        self.d_off = torch.empty(2 * max_pkts, dtype=torch.int64, device=dev)
+        self.d_len = torch.empty(2 * max_pkts, dtype=torch.int32, device=dev)
+        self.d_first = torch.empty(max_pkts + 1, dtype=torch.int32, device=dev)
+        self.d_status = torch.empty(max_pkts, dtype=torch.uint8, device=dev)
+        self.done = torch.cuda.Event()
+
+    def close(self):
+        for b in (self.host, self.h_off, self.h_len, self.h_first, self.h_status):
+            b.free()
+
+
+class TxChainPipeline:
+    """Batched transmit of NetBuffer chains: the caller writes each
+    datagram's head fragment — IP header then L4 header, checksum fields unset, as
+    alloc_header leaves them (buf.rs:262-291) — back to back into ``heads()`` and its payload
+    at a 16-byte-aligned offset of its choice into ``payloads()``, then ``send`` (or
+    ``submit`` / ``complete``) with the head lengths and the payload offsets and lengths.
+    One H2D copy of the used header bytes and one of the used payload bytes ->
+    rns_tx_fill_chain_dev (pseudo-headers, L4 and IPv4 header checksums stored into the
+    heads) -> D2H of the header region only -> rns_io_send_batch_chain (each datagram
+    gathered from [head, payload], as send_packet's to_iovec + writev send a NetBuffer,
+    netif.rs:51-98)."""
+
+    HEAD_MAX = 128  # bytes per head fragment, at most (IPv4 with options + TCP with options)
+    DEPTH = 2
+
+    def __init__(self, device: int = 0, max_pkts: int = 65536, payload_bytes: int | None = None):
+        self.max_pkts = max_pkts
+        self.dev = torch.device(f"cuda:{device}")
+        self.head_region = (self.HEAD_MAX * max_pkts + 4095) & ~4095
+        self.payload_bytes = payload_bytes if payload_bytes is not None else MRU * max_pkts
+        self._sets = [_ChainSet(self.dev, max_pkts, self.head_region, self.payload_bytes) for _ in range(self.DEPTH)]
+        self._next = 0
+        self._inflight: deque = deque()
+        self._stream = None
+
+    def heads(self) -> np.ndarray:
+        """The free set's header region: head fragments back to back in datagram order."""
+        if len(self._inflight) == self.DEPTH:
+            raise RuntimeError("every buffer set is in flight: complete() one first")
+        return self._sets[self._next].host.array[: self.head_region]
+
+    def payloads(self) -> np.ndarray:
+        """The free set's payload region (offsets passed to send / submit are relative to it)."""
+        if len(self._inflight) == self.DEPTH:
+            raise RuntimeError("every buffer set is in flight: complete() one first")
+        return self._sets[self._next].host.array[self.head_region: self.head_region + self.payload_bytes]
+
+    def pending(self) -> int:
+        return len(self._inflight)
+
+    def _describe(self, s: _ChainSet, head_len, pay_off, pay_len):
+        """Chain descriptors [head, payload (if any)] per datagram into the set's pinned arrays;
+        returns (n, fragments, header bytes used, payload bytes used)."""
+        hl = np.ascontiguousarray(head_len, dtype=np.int64)
+        po = np.ascontiguousarray(pay_off, dtype=np.int64)
+        pl = np.ascontiguousarray(pay_len, dtype=np.int64)
+        n = hl.shape[0]
+        if po.shape[0] != n or pl.shape[0] != n:
+            raise ValueError("head_len, pay_off and pay_len need one entry per datagram")
+        if n > self.max_pkts:
+            raise ValueError("more datagrams than the pipeline holds")
+        if n and (hl.min() < 1 or hl.max() > self.HEAD_MAX or pl.min() < 0 or po.min() < 0 or
+                  int((po + pl).max()) > self.payload_bytes):
+            raise ValueError(f"head lengths must be 1..{self.HEAD_MAX} and payloads inside payloads()")
+        hoff = np.zeros(n, dtype=np.int64)
+        if n > 1:
+            np.cumsum(hl[:-1], out=hoff[1:])
+        nfr = 1 + (pl > 0)
+        first = s.h_first.array.view(np.uint32)[: n + 1]
+        first[0] = 0
+        first[1:] = np.cumsum(nfr)
+        nf = int(first[n])
+        off = s.h_off.array.view(np.uint64)[:nf]
+        ln = s.h_len.array.view(np.uint32)[:nf]
+        f0 = first[:n].astype(np.int64)
+        off[f0] = hoff.astype(np.uint64)
+        ln[f0] = hl.astype(np.uint32)
+        has = pl > 0
+        off[f0[has] + 1] = (po[has] + self.head_region).astype(np.uint64)
+        ln[f0[has] + 1] = pl[has].astype(np.uint32)
+        hused = int(hoff[-1] + hl[-1]) if n else 0
+        pused = int((po + pl).max()) if n else 0
+        return n, nf, hused, pused
+
+    def _queue(self, s: _ChainSet, n: int, nf: int, hused: int, pused: int) -> None:
+        hr = self.head_region
+        s.d_arena[:hused].copy_(torch.from_numpy(s.host.array[:hused]), non_blocking=True)
+        if pused:
+            s.d_arena[hr:hr + pused].copy_(torch.from_numpy(s.host.array[hr:hr + pused]), non_blocking=True)
+        s.d_off[:nf].copy_(torch.from_numpy(s.h_off.array.view(np.int64)[:nf]), non_blocking=True)
+        s.d_len[:nf].copy_(torch.from_numpy(s.h_len.array.view(np.int32)[:nf]), non_blocking=True)
+        s.d_first[:n + 1].copy_(torch.from_numpy(s.h_first.array.view(np.int32)[:n + 1]), non_blocking=True)
+        tx_fill_chain(s.d_arena, s.d_off[:nf], s.d_len[:nf], s.d_first[:n + 1], status=s.d_status[:n])
+        torch.from_numpy(s.host.array[:hused]).copy_(s.d_arena[:hused], non_blocking=True)
+        torch.from_numpy(s.h_status.array[:n]).copy_(s.d_status[:n], non_blocking=True)
+        s.done.record()
+
+    def _finish(self, fd: int, s: _ChainSet, n: int, nf: int) -> np.ndarray:
+        s.done.synchronize()
+        sent = send_batch_chain(fd, s.host.array, s.h_off.array.view(np.uint64)[:nf],
+                                s.h_len.array.view(np.uint32)[:nf], s.h_first.array.view(np.uint32)[:n + 1])
+        if sent != n:
+            raise OSError(f"sent {sent} of {n} datagrams")
+        return s.h_status.array[:n].copy()
+
+    def send(self, fd: int, head_len, pay_off, pay_len) -> np.ndarray:
+        """Finalize and send datagrams [0, n) of ``heads()`` / ``payloads()``; returns their
+        RNS_TX_* status."""
+        if self._inflight:
+            raise RuntimeError("submitted batches pending: complete() them first")
+        s = self._sets[self._next]
+        n, nf, hused, pused = self._describe(s, head_len, pay_off, pay_len)
+        if n == 0:
+            return np.empty(0, dtype=np.uint8)
+        with torch.cuda.device(self.dev):
+            self._queue(s, n, nf, hused, pused)
+        return self._finish(fd, s, n, nf)
+
+    def submit(self, head_len, pay_off, pay_len) -> None:
+        """Queue the GPU work for the free set's datagrams and hand out the other set."""
+        if len(self._inflight) == self.DEPTH:
+            raise RuntimeError("every buffer set is in flight: complete() one first")
+        s = self._sets[self._next]
+        n, nf, hused, pused = self._describe(s, head_len, pay_off, pay_len)
+        with torch.cuda.device(self.dev):
+            if self._stream is None:
+                self._stream = torch.cuda.Stream(self.dev)
+            with torch.cuda.stream(self._stream):
+                if n:
+                    self._queue(s, n, nf, hused, pused)
+                else:
+                    s.done.record()
+        self._inflight.append((s, n, nf))
+        self._next = (self._next + 1) % self.DEPTH
+
+    def complete(self, fd: int) -> np.ndarray:
+        """Wait for the oldest submitted batch, send it; returns its RNS_TX_* status."""
+        if not self._inflight:
+            raise RuntimeError("nothing submitted")
+        s, n, nf = self._inflight.popleft()
+        if n == 0:
+            return np.empty(0, dtype=np.uint8)
+        return self._finish(fd, s, n, nf)
 
     def close(self):
         for s in self._sets:

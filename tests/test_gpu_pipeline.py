@@ -175,3 +175,70 @@ def test_tx_overlapped_to_socket(oracle):
     assert len(received) == len(pkts)
     bad = [i for i in range(len(pkts)) if received[i] != want[i][0]]
     assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_tx_chain_pipeline_to_socket(oracle, overlap):
+    """TxChainPipeline: every kind of outgoing datagram as the reference builds it — a head
+    fragment (IP + L4 headers, alloc_header) in the header region and its payload in the payload
+    region — finalized on the GPU and sent gathered from its two fragments (send_packet's
+    writev); the far end receives exactly the contiguous datagram the reference's transmit path
+    would send (oracle.tx_chain_fill_ref == tx_fill_ref for an even L4 header part), in order."""
+    from rustnetworkstack_amd.batch import recv_batch
+    from rustnetworkstack_amd.pipeline import TxChainPipeline
+    from test_gpu_tx import outgoing
+    from test_gpu_tx_chain import l4_header_len
+    pkts = [p for p in outgoing(4000, 0x7C4A + overlap) if 0 < len(p) <= 2048]
+    heads = [p[:min(len(p), l4_header_len(p), TxChainPipeline.HEAD_MAX)] for p in pkts]
+    want = []
+    for p, h in zip(pkts, heads):
+        frags = [h] + ([p[len(h):]] if len(p) > len(h) else [])
+        hh, st = O.tx_chain_fill_ref(frags, ones_comp=oracle.compute_ones_comp)
+        want.append((hh + p[len(h):], st))
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+    for s_, opt in ((a, socket.SO_SNDBUF), (b, socket.SO_RCVBUF)):
+        s_.setsockopt(socket.SOL_SOCKET, opt, 32 << 20)
+    received = []
+
+    def drain():
+        buf = np.empty(2048 * 1024, dtype=np.uint8)
+        while len(received) < len(pkts):
+            off, ln = recv_batch(b.fileno(), buf, 2048, 1024, timeout_ms=5000)
+            if ln.shape[0] == 0:
+                return
+            received.extend(buf[int(o):int(o) + int(n)].tobytes() for o, n in zip(off, ln))
+
+    t = threading.Thread(target=drain)
+    t.start()
+    pipe = TxChainPipeline(device=0, max_pkts=600)
+    statuses = []
+    for i0 in range(0, len(pkts), 600):
+        if overlap and pipe.pending() == pipe.DEPTH:
+            statuses.append(pipe.complete(a.fileno()))
+        chunk = range(i0, min(i0 + 600, len(pkts)))
+        hreg, preg = pipe.heads(), pipe.payloads()
+        hl, po, pl = [], [], []
+        hpos = ppos = 0
+        for i in chunk:
+            h, body = heads[i], pkts[i][len(heads[i]):]
+            hreg[hpos:hpos + len(h)] = np.frombuffer(h, dtype=np.uint8)
+            preg[ppos:ppos + len(body)] = np.frombuffer(body, dtype=np.uint8)
+            hl.append(len(h))
+            po.append(ppos)
+            pl.append(len(body))
+            hpos += len(h)
+            ppos = (ppos + len(body) + 15) & ~15
+        if overlap:
+            pipe.submit(np.array(hl), np.array(po), np.array(pl))
+        else:
+            statuses.append(pipe.send(a.fileno(), np.array(hl), np.array(po), np.array(pl)))
+    while pipe.pending():
+        statuses.append(pipe.complete(a.fileno()))
+    t.join(timeout=60)
+    pipe.close()
+    a.close()
+    b.close()
+    assert np.array_equal(np.concatenate(statuses), np.array([w[1] for w in want], dtype=np.uint8))
+    assert len(received) == len(pkts)
+    bad = [i for i in range(len(pkts)) if received[i] != want[i][0]]
+    assert not bad, bad[:5]

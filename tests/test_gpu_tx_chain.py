@@ -173,7 +173,7 @@ def test_chain_finalize_equals_contiguous_fill_for_even_pieces():
     off2[hidx] += 20
     ln2[hidx] -= 20
     seg = np.array([len(pkts[i]) - 20 for i in np.flatnonzero(keep)])
-    seeds = np.array([O.pseudo_header_py(R4, L4, s, 6) for s in seg], dtype=np.uint16)
+    seeds = np.array([O.pseudo_header_py(R4, L4, int(s), 6) for s in seg], dtype=np.uint16)
     cnt = (first[1:] - first[:-1])[keep].astype(np.int64)
     f2 = np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint32)
     fr = np.repeat(hidx.astype(np.int64), cnt) + (np.arange(int(cnt.sum())) - np.repeat(f2[:-1].astype(np.int64), cnt))
@@ -233,7 +233,9 @@ def test_chain_finalize_full_size_then_receive(oracle, name, frag):
     a[idx.flatten()] = torch.from_numpy(hdr).to(DEV).repeat(lay.n)
     del idx
     sample = 3000
-    s_end = int(lay.frag_off[first[sample] - 1] + lay.frag_len[first[sample] - 1])
+    # (the sample's fragments end anywhere below the last one's: a head-only datagram's last
+    # fragment is its head, in the header region)
+    s_end = int((lay.frag_off[:first[sample]] + lay.frag_len[:first[sample]].astype(np.uint64)).max())
     before = a[:s_end].cpu().numpy()
     d_off, d_len, d_first = dev(lay.frag_off, np.int64), dev(lay.frag_len, np.int32), dev(lay.first, np.int32)
     st = tx_fill_chain(a, d_off, d_len, d_first)

@@ -6,7 +6,10 @@ import socket
 import numpy as np
 
 from oracle import oracle as O
-from rustnetworkstack_amd.batch import recv_batch, send_batch
+import pytest
+
+from rustnetworkstack_amd import _lib
+from rustnetworkstack_amd.batch import recv_batch, send_batch, send_batch_chain
 
 
 def make(n, seed, maxlen=2100):
@@ -118,5 +121,53 @@ def test_send_batch_large_batches_keep_order():
     assert np.array_equal(ln, lens)
     assert all(slots[512 * j:512 * j + int(n)].tobytes() == arena[int(off[j]):int(off[j]) + int(n)].tobytes()
                for j, n in enumerate(ln))
+    a.close()
+    b.close()
+
+
+def test_send_batch_chain_gathers_each_datagram():
+    """rns_io_send_batch_chain: each datagram leaves as ONE datagram gathered from its fragments
+    (send_packet's to_iovec + writev, netif.rs:51-98): heads in one region, payload pieces
+    elsewhere, 1-8 fragments, empty pieces; 700 datagrams in order."""
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+    a.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 1 << 23)
+    b.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 23)
+    n = 700
+    w = O.splitmix64_words(0x5EC4, 3 * n)
+    arena = O.splitmix64_bytes(0x5EC5, 1 << 20)
+    off, ln, first, want = [], [], [0], []
+    hpos, ppos = 0, 200_000
+    for i in range(n):
+        k = 1 + int(w[i] % np.uint64(_lib.RNS_IO_MAX_FRAGS))
+        parts = []
+        for j in range(k):
+            L = 40 if j == 0 else int((w[n + i] >> np.uint64(8 * j)) % np.uint64(300))
+            o = hpos if j == 0 else ppos
+            if j == 0:
+                hpos += L
+            else:
+                ppos += L + int(w[2 * n + i] % np.uint64(7))
+            off.append(o)
+            ln.append(L)
+            parts.append(arena[o:o + L].tobytes())
+        first.append(len(off))
+        want.append(b"".join(parts))
+    assert send_batch_chain(a.fileno(), arena, np.array(off, np.uint64), np.array(ln, np.uint32),
+                            np.array(first, np.uint32)) == n
+    slots = np.zeros(4096 * n, dtype=np.uint8)
+    o, got_len = recv_batch(b.fileno(), slots, 4096, timeout_ms=1000)
+    assert got_len.shape[0] == n
+    assert all(slots[int(o[j]):int(o[j]) + int(got_len[j])].tobytes() == want[j] for j in range(n))
+    # an empty chain or more than RNS_IO_MAX_FRAGS fragments: nothing is sent
+    for bad_first in ([0, 1, 1], [0, 9]):
+        with pytest.raises(_lib.ChecksumError):
+            send_batch_chain(a.fileno(), arena, np.zeros(9, np.uint64), np.ones(9, np.uint32),
+                             np.array(bad_first, np.uint32))
+    with pytest.raises(ValueError):
+        send_batch_chain(a.fileno(), arena, np.array([arena.size - 4], np.uint64), np.array([8], np.uint32),
+                         np.array([0, 1], np.uint32))
+    b.setblocking(False)
+    with pytest.raises(BlockingIOError):
+        b.recv(10)
     a.close()
     b.close()

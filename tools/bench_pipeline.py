@@ -9,6 +9,10 @@ H2D of whole slots -> rns_rx_verify_dev).
 Transmit (--tx): the same datagrams with their checksum fields zeroed are placed in
 TxPipeline's pinned slots and sent (H2D -> rns_tx_fill_dev -> header bytes D2H ->
 rns_io_send_batch); a drain thread reads them and the result is spot-checked.
+Transmit chains (--tx --chain): each datagram as the reference builds it — a 40-byte head
+fragment (IPv4 + TCP headers) in TxChainPipeline's header region, its 1460-byte payload in the
+payload region (H2D of the used bytes -> rns_tx_fill_chain_dev -> the header region D2H ->
+rns_io_send_batch_chain, each datagram gathered from its two fragments).
 
     python tools/bench_pipeline.py [--packets 262144] [--batch 8192] [--tx] [--overlap]
 
@@ -31,7 +35,7 @@ import torch  # noqa: E402
 
 from rustnetworkstack_amd.batch import send_batch  # noqa: E402
 from rustnetworkstack_amd.batch import recv_batch  # noqa: E402
-from rustnetworkstack_amd.pipeline import RxPipeline, TxPipeline  # noqa: E402
+from rustnetworkstack_amd.pipeline import RxPipeline, TxChainPipeline, TxPipeline  # noqa: E402
 from rustnetworkstack_amd.workloads import DeviceBatch, make_layout  # noqa: E402
 from bench_ops import L4, L6, write_ipv4_tcp_headers  # noqa: E402
 
@@ -43,6 +47,7 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--tx", action="store_true")
     ap.add_argument("--overlap", action="store_true")
+    ap.add_argument("--chain", action="store_true", help="with --tx: TxChainPipeline (head + payload fragments)")
     ap.add_argument("--slots", action="store_true", help="receive into 2048-B slots (round-5 form)")
     ap.add_argument("--config", default="c3_1500B", help="datagram sizes: c3_1500B or c2_64B")
     args = ap.parse_args()
@@ -110,7 +115,7 @@ def main_tx(args):
     a, r = socket.socketpair(socket.AF_UNIX, socket.SOCK_SEQPACKET)
     for s_, opt in ((a, socket.SO_SNDBUF), (r, socket.SO_RCVBUF)):
         s_.setsockopt(socket.SOL_SOCKET, opt, 64 << 20)
-    pipe = TxPipeline(device=0, max_pkts=args.batch)
+    pipe = TxChainPipeline(device=0, max_pkts=args.batch) if args.chain else TxPipeline(device=0, max_pkts=args.batch)
     got = [0]
     sample = {}
 
@@ -132,21 +137,30 @@ def main_tx(args):
         k = min(args.batch, n - i0)
         if args.overlap and pipe.pending() == pipe.DEPTH:
             filled += int((pipe.complete(a.fileno()) == 3).sum())
-        pipe.slots()[:k, :1500] = unfilled[i0:i0 + k]
-        if args.overlap:
-            pipe.submit(np.full(k, 1500, dtype=np.uint32))
+        if args.chain:  # heads back to back, payloads at 16-byte steps (1472 B)
+            pipe.heads()[:40 * k] = unfilled[i0:i0 + k, :40].reshape(-1)
+            pipe.payloads()[:1472 * k].reshape(k, 1472)[:, :1460] = unfilled[i0:i0 + k, 40:]
+            desc = (np.full(k, 40), np.arange(k) * 1472, np.full(k, 1460))
         else:
-            filled += int((pipe.send(a.fileno(), np.full(k, 1500, dtype=np.uint32)) == 3).sum())
+            pipe.slots()[:k, :1500] = unfilled[i0:i0 + k]
+            desc = (np.full(k, 1500, dtype=np.uint32),)
+        if args.overlap:
+            pipe.submit(*desc)
+        else:
+            filled += int((pipe.send(a.fileno(), *desc) == 3).sum())
     while pipe.pending():
         filled += int((pipe.complete(a.fileno()) == 3).sum())
     t.join()
     dt = time.perf_counter() - t0
     exact = all(np.array_equal(v, dgrams[i]) for i, v in sample.items())
-    res = {"direction": "transmit", "overlap": args.overlap, "packets": n, "received": got[0], "filled": filled,
+    res = {"direction": "transmit", "chain": args.chain, "overlap": args.overlap, "packets": n, "received": got[0], "filled": filled,
            "sample_exact": exact, "sampled": len(sample), "seconds": round(dt, 3),
            "packets_per_s": round(got[0] / dt), "GBps": round(got[0] * 1500 / dt / 1e9, 3),
-           "path": "host datagrams -> pinned 2048-B slots -> H2D -> rns_tx_fill_dev -> 128 B/slot D2H -> "
-                   "rns_io_send_batch -> AF_UNIX SOCK_SEQPACKET socketpair; drain on another host thread"}
+           "path": ("host chains [40 B head, 1460 B payload] -> pinned header / payload regions -> H2D of the used "
+                    "bytes -> rns_tx_fill_chain_dev -> header region D2H -> rns_io_send_batch_chain (sendmmsg, "
+                    "two iovecs per datagram)" if args.chain else
+                    "host datagrams -> pinned 2048-B slots -> H2D -> rns_tx_fill_dev -> 128 B/slot D2H -> "
+                    "rns_io_send_batch") + " -> AF_UNIX SOCK_SEQPACKET socketpair; drain on another host thread"}
     print(json.dumps(res))
     if args.out:
         with open(args.out, "w") as f:
