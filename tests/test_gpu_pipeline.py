@@ -189,7 +189,7 @@ def test_tx_chain_pipeline_to_socket(oracle, overlap):
     from test_gpu_tx import outgoing
     from test_gpu_tx_chain import l4_header_len
     pkts = [p for p in outgoing(4000, 0x7C4A + overlap) if 0 < len(p) <= 2048]
-    heads = [p[:min(len(p), l4_header_len(p), TxChainPipeline.HEAD_MAX)] for p in pkts]
+    heads = [p[:min(len(p), max(1, l4_header_len(p)), TxChainPipeline.HEAD_MAX)] for p in pkts]  # (garbage: IHL 0)
     want = []
     for p, h in zip(pkts, heads):
         frags = [h] + ([p[len(h):]] if len(p) > len(h) else [])
