@@ -506,19 +506,8 @@ __global__ __launch_bounds__(64, kStridedRxOcc) void csum_strided_rx_kernel(cons
                 const uint32_t c0x = dpp_mov<0x00>(xm.x), c0y = dpp_mov<0x00>(xm.y);  // chunk 0 (quad lane 0)
                 const uint32_t c0z = dpp_mov<0x00>(xm.z), c0w = dpp_mov<0x00>(xm.w);
                 const uint32_t c1x = dpp_mov<0x55>(xm.x), c1y = dpp_mov<0x55>(xm.y);  // chunk 1 (quad lane 1)
-                const uint32_t b0 = c0x & 0xffu, v = b0 >> 4;
-                const uint32_t hdr = v == 4 ? (b0 & 15u) * 4u : v == 6 ? 40u : 0u;  // <= 60
-                uint4 hm = make_uint4(0, 0, 0, 0);
-                if (16u * j < hdr)
-                    hm = 16u * j + 16u <= hdr ? xm : keep_first(xm, hdr - 16u * j);
-                uint32_t h = __builtin_amdgcn_sad_u16(hm.x, 0, 0u);
-                h = __builtin_amdgcn_sad_u16(hm.y, 0, h);
-                h = __builtin_amdgcn_sad_u16(hm.z, 0, h);
-                h = __builtin_amdgcn_sad_u16(hm.w, 0, h);
-                h = group_allreduce<4>(h);
                 if (j == static_cast<uint32_t>(r)) {
                     mine = t;
-                    H = h;
                     head[0] = c0x;
                     head[1] = c0y;
                     head[2] = c0z;
@@ -531,6 +520,35 @@ __global__ __launch_bounds__(64, kStridedRxOcc) void csum_strided_rx_kernel(cons
             row(std::integral_constant<int, 1>{});
             row(std::integral_constant<int, 2>{});
             row(std::integral_constant<int, 3>{});
+            // H, the header's word sum (IHL*4 bytes, or 40 for IPv6): from the owner's first 20
+            // bytes when no datagram of the wave has a longer header (IPv4 without options, the
+            // ACK case), else per row from the quad's chunks like T
+            const uint32_t hb0 = head[0] & 0xffu, hv = hb0 >> 4;
+            const uint32_t hdr = hv == 4 ? (hb0 & 15u) * 4u : hv == 6 ? 40u : 0u;  // <= 60
+            if (!__ballot(present && hdr > 20u)) {
+#pragma unroll
+                for (uint32_t d = 0; d < 5; ++d)
+                    H = __builtin_amdgcn_sad_u16(4u * d < hdr ? head[d] : 0u, 0, H);
+            } else {
+                auto hrow = [&](auto rc) {
+                    constexpr int r = decltype(rc)::value;
+                    const uint32_t hr = dpp_mov<r * 0x55>(hdr);  // the row's datagram's header length
+                    const uint4 xv = x[b][r];
+                    uint4 hm = make_uint4(0, 0, 0, 0);
+                    if (16u * j < hr)
+                        hm = 16u * j + 16u <= hr ? xv : keep_first(xv, hr - 16u * j);
+                    uint32_t h = __builtin_amdgcn_sad_u16(hm.x, 0, 0u);
+                    h = __builtin_amdgcn_sad_u16(hm.y, 0, h);
+                    h = __builtin_amdgcn_sad_u16(hm.z, 0, h);
+                    h = __builtin_amdgcn_sad_u16(hm.w, 0, h);
+                    h = group_allreduce<4>(h);
+                    H = j == static_cast<uint32_t>(r) ? h : H;
+                };
+                hrow(std::integral_constant<int, 0>{});
+                hrow(std::integral_constant<int, 1>{});
+                hrow(std::integral_constant<int, 2>{});
+                hrow(std::integral_constant<int, 3>{});
+            }
             uint64_t todo = __ballot(present && L > 64);
             while (todo) {  // longer datagrams: the whole wave sums one at a time
                 const uint32_t o = static_cast<uint32_t>(__builtin_ctzll(todo));
