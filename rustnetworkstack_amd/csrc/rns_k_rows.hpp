@@ -1075,6 +1075,8 @@ __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const C
     // stages its raw head chunks in LDS, patches its fields there and writes the run's whole
     // 16-byte chunks back (full 64-byte segments, about half the write requests of two field
     // stores per head); fields in the run's partial edge chunks take the 2-byte stores.
+    // (the same write-back for the one-field fill measured no gain: c3 246.8 / IMIX 598.0 us against
+    // 246.1 / 597.8, session r06n — its 20-byte heads already leave one request per 64-byte segment)
     constexpr bool kRunWrite = FIN && RNS_TXFIN_RUNWRITE != 0;
     bool runw = false;
     uint64_t b0 = 0, r1 = 0;  // the run's first chunk boundary, its end
@@ -1107,18 +1109,18 @@ __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const C
         uint32_t acc1 = 0;
         auto head = [&]() {
             uint32_t hsum = 0, sd = seed;
+            if constexpr (kRunWrite) {
+                if (runw) {  // the raw chunks the head touches (neighbours' bytes in them are raw too)
+                    const uint32_t q = static_cast<uint32_t>((hb - b0) >> 4);
+#pragma unroll
+                    for (uint32_t i = 0; i < kNH; ++i)
+                        if (16u * i < span)
+                            run_lds[q + i] = h[i];
+                }
+            }
             if constexpr (FIN) {
                 uint32_t hd;
                 fst = chain_tx_head<kNH>(h, hs, hl, hl + plen, (o[0] & 1u) != 0, live && !bad, ipv, l4f, hsum, sd, hd);
-                if constexpr (kRunWrite) {
-                    if (runw) {  // the raw chunks the head touches (neighbours' bytes in them are raw too)
-                        const uint32_t q = static_cast<uint32_t>((hb - b0) >> 4);
-#pragma unroll
-                        for (uint32_t i = 0; i < kNH; ++i)
-                            if (16u * i < span)
-                                run_lds[q + i] = h[i];
-                    }
-                }
             } else {
 #pragma unroll
             for (uint32_t i = 0; i < 4; ++i) {
@@ -1242,61 +1244,63 @@ __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const C
     }
     const bool okp = live && !bad;
     const uint32_t r = (FIN || (a.flags & RNS_FLAG_COMPLEMENT)) ? res ^ 0xffffu : res;
-    if constexpr (FIN) {  // set_be16 into header_mut(): the L4 field, then ip.rs:158-159's
-        const bool s4 = okp && (fst & RNS_TX_L4_FILLED), s3 = okp && (fst & RNS_TX_IP_FILLED);
-        uint64_t c0w = 0, c1w = 0;  // the run's whole chunks [c0w, c1w) (run write-back)
-        if constexpr (kRunWrite) {
-            if (runw) {
-                uint8_t *l8 = reinterpret_cast<uint8_t *>(run_lds);
-                const uint64_t q = o[0] - b0;
-                if (s4) {
-                    l8[q + l4f] = static_cast<uint8_t>(r >> 8);
-                    l8[q + l4f + 1] = static_cast<uint8_t>(r);
+    // the fields to store (set_be16 into header_mut()): FIN the L4 field, then ip.rs:158-159's
+    // IPv4 header checksum; FILL the caller's field
+    constexpr uint64_t kNoPos = ~0ull;
+    uint64_t fpos[2] = {kNoPos, kNoPos};
+    uint32_t fval[2] = {0u, 0u};
+    if constexpr (FIN) {
+        if (okp && (fst & RNS_TX_L4_FILLED)) {
+            fpos[0] = o[0] + l4f;
+            fval[0] = r;
+        }
+        if (okp && (fst & RNS_TX_IP_FILLED)) {
+            fpos[1] = o[0] + 10;
+            fval[1] = ipv;
+        }
+    }
+    if constexpr (FILL) {
+        if (okp) {
+            fpos[0] = o[0] + fo;
+            fval[0] = r;
+        }
+    }
+    uint64_t c0w = 0, c1w = 0;  // the run's whole chunks [c0w, c1w) (run write-back)
+    if constexpr (kRunWrite) {
+        if (runw) {
+            uint8_t *l8 = reinterpret_cast<uint8_t *>(run_lds);
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (fpos[k] != kNoPos) {
+                    l8[fpos[k] - b0] = static_cast<uint8_t>(fval[k] >> 8);
+                    l8[fpos[k] - b0 + 1] = static_cast<uint8_t>(fval[k]);
                 }
-                if (s3) {
-                    l8[q + 10] = static_cast<uint8_t>(ipv >> 8);
-                    l8[q + 11] = static_cast<uint8_t>(ipv);
-                }
-                __syncthreads();
-                c0w = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(o[0] & 15u)) == 0 ? b0 : b0 + 16;
-                c1w = r1 & ~15ull;
-                uint8_t *w8 = const_cast<uint8_t *>(a.arena);
-                for (uint64_t c = c0w + 16u * lane; c < c1w; c += 1024u) {
-                    const uint4 v = run_lds[(c - b0) >> 4];
-                    if constexpr (BUF) {
-                        const u32x4 y = {v.x, v.y, v.z, v.w};
-                        __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, static_cast<uint32_t>(c), 0, RNS_STREAM_OUT_AUX);
-                    } else {
-                        *reinterpret_cast<uint4 *>(w8 + c) = v;
-                    }
+            }
+            __syncthreads();
+            c0w = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(o[0] & 15u)) == 0 ? b0 : b0 + 16;
+            c1w = r1 & ~15ull;
+            uint8_t *w8 = const_cast<uint8_t *>(a.arena);
+            for (uint64_t c = c0w + 16u * lane; c < c1w; c += 1024u) {
+                const uint4 v = run_lds[(c - b0) >> 4];
+                if constexpr (BUF) {
+                    const u32x4 y = {v.x, v.y, v.z, v.w};
+                    __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, static_cast<uint32_t>(c), 0, RNS_STREAM_OUT_AUX);
+                } else {
+                    *reinterpret_cast<uint4 *>(w8 + c) = v;
                 }
             }
         }
-        // (with the run write-back, only the fields not wholly inside its chunks)
-        auto outside = [&](uint64_t fp) { return !runw || fp < c0w || fp + 2 > c1w; };
-        if (s4 && outside(o[0] + l4f))
-            store_field<BUF, RNS_STREAM_OUT_AUX>(a, rsrc, o[0] + l4f, r);
-        if (s3 && outside(o[0] + 10))
-            store_field<BUF, RNS_STREAM_OUT_AUX>(a, rsrc, o[0] + 10, ipv);
-        if (live && a.status)
-            a.status[p] = okp ? static_cast<uint8_t>(fst) : static_cast<uint8_t>(RNS_TX_MALFORMED);
     }
     // (field stores as buffer stores with the result stores' sc0|sc1 bits: IMIX 604.4 -> 598.4 us,
-    // c3 251.0 -> 245.7 against ordinary stores; nontemporal 595.8 / 246.4: session r05e)
-    if constexpr (FILL) {
-        if (okp) {  // set_be16(&mut header[fo..fo + 2], result): the head fragment's bytes
-            uint8_t *w8 = const_cast<uint8_t *>(a.arena);
-            const uint64_t fp = o[0] + fo;
-            if (fp & 1) {
-                w8[fp] = static_cast<uint8_t>(r >> 8);
-                w8[fp + 1] = static_cast<uint8_t>(r);
-            } else if (BUF) {
-                __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(bswap16_u32(r & 0xffffu)), rsrc,
-                                                      static_cast<uint32_t>(fp), 0, RNS_STREAM_OUT_AUX);
-            } else {
-                *reinterpret_cast<uint16_t *>(w8 + fp) = static_cast<uint16_t>(bswap16_u32(r & 0xffffu));
-            }
-        }
+    // c3 251.0 -> 245.7 against ordinary stores; nontemporal 595.8 / 246.4: session r05e; with the
+    // run write-back only the fields not wholly inside its chunks)
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        if (fpos[k] != kNoPos && (!runw || fpos[k] < c0w || fpos[k] + 2 > c1w))
+            store_field<BUF, RNS_STREAM_OUT_AUX>(a, rsrc, fpos[k], fval[k]);
+    if constexpr (FIN) {
+        if (live && a.status)
+            a.status[p] = okp ? static_cast<uint8_t>(fst) : static_cast<uint8_t>(RNS_TX_MALFORMED);
     }
     if (live && a.out) {
         const uint16_t v = okp ? static_cast<uint16_t>(r) : static_cast<uint16_t>(0);
