@@ -49,6 +49,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip-level 
 METRIC = "GiB/s device-resident Internet checksum, 1500B-packet batches, 1/2/4/8 GPUs"
 # --op verify (not the headline): receive verify of IPv4/TCP datagrams (rns_rx_verify_dev)
 METRIC_VERIFY = "GiB/s device-resident receive verify (ip.rs:76 + tcp.rs:838-850), IPv4/TCP datagrams"
+# --op finalize (not the headline): transmit finalize of NetBuffer chains (rns_tx_fill_chain_dev)
+METRIC_FINALIZE = ("GiB/s device-resident transmit finalize (tcp.rs:957-973 + ip.rs:140-160) of NetBuffer chains, "
+                   "IPv4/TCP datagrams")
 
 
 def parse_args(argv=None):
@@ -57,11 +60,14 @@ def parse_args(argv=None):
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="c3_1500B")
-    p.add_argument("--op", choices=("csum", "verify"), default="csum",
+    p.add_argument("--op", choices=("csum", "verify", "finalize"), default="csum",
                    help="csum (the headline): the batch checksum, per-packet seed, complemented result; verify: "
                         "every packet is an IPv4/TCP datagram (checksums filled by rns_tx_fill_dev, every 1009th "
                         "corrupted) and a step is one rns_rx_verify_dev launch; at N>1 the SURVEY §8(e) leg is an "
-                        "all-reduce(sum) of the per-rank rejected-datagram counts instead of the result all-gather")
+                        "all-reduce(sum) of the per-rank rejected-datagram counts instead of the result all-gather; "
+                        "finalize: every packet is an outgoing IPv4/TCP datagram held as a NetBuffer chain [40-byte "
+                        "head fragment, payload] (heads in a header region) and a step is one rns_tx_fill_chain_dev "
+                        "launch (both checksums stored into every head); nothing is exchanged between ranks")
     p.add_argument("--desc", choices=("auto", "64", "32", "packed", "strided"), default="auto",
                    help="descriptor form: 64 = u64 offsets (rns_csum_batch_dev); 32 = u32 offsets "
                         "(rns_csum_batch_dev_off32); packed = u16 lengths + one offset per 64 packets "
@@ -111,6 +117,8 @@ def parse_args(argv=None):
         p.error("--op verify takes the packed form (rns_rx_verify_packed_dev), the strided form "
                 "(rns_rx_verify_strided_dev; auto for tiny datagrams in fixed-size slots) or 64-bit descriptors "
                 "(rns_rx_verify_dev) and the receive kernel's own shape")
+    if args.op == "finalize" and (args.shape or args.desc != "auto"):
+        p.error("--op finalize takes the chain form (rns_tx_fill_chain_dev) and its kernel's own shape")
     args.shard_rw = None
     if args.shard:
         try:
@@ -398,6 +406,9 @@ class GpuEngine:
             return make_layout(config, data_seed=DATA_SEED + 0x1000 * rank + r)
 
         self.op = op
+        if op == "finalize":
+            self._init_finalize(config, rank, world, strong, min_batches)
+            return
         self.layout = layout(0)
         small = self.layout.arena_bytes < (512 << 20)
         # Rotating batches, each with its own bytes (cache honesty):
@@ -450,6 +461,32 @@ class GpuEngine:
         self.gatherer = None
         torch.cuda.synchronize()
 
+    def _init_finalize(self, config, rank, world, strong, min_batches):
+        """--op finalize: rotating transmit batches held as NetBuffer chains (workloads.TxChainBatch)."""
+        torch = self.torch
+        from rustnetworkstack_amd.workloads import DATA_SEED, TxChainBatch
+
+        def batch(r):
+            seed = DATA_SEED + 0x1000 * rank + r
+            return TxChainBatch(config, self.device, data_seed=seed, shard=(rank, world) if strong else (0, 1))
+
+        b0 = batch(0)
+        self.layout = b0.layout
+        nrot = max(1, -(-(768 << 20) // max(self.layout.arena_bytes, 1))) if self.layout.arena_bytes < (512 << 20) else 1
+        nrot = max(nrot, int(min_batches))
+        self.batches = [b0] + [batch(r) for r in range(1, nrot)]
+        self.shape = None
+        self.form = "chain"
+        self.compact = self.packed = self.strided = False
+        self.verify_packed = self.verify_strided = False
+        self.k = 0
+        self.used = set()
+        self.last = self.batches[0]
+        self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        self.timed = 0
+        self.gatherer = None
+        torch.cuda.synchronize()
+
     @property
     def n(self):
         return self.layout.n
@@ -470,11 +507,17 @@ class GpuEngine:
             return lambda: rx_verify_packed(b.arena, b.blk_off, b.len16, LOCAL4, LOCAL6, status=b.status)
         return lambda: rx_verify(b.arena, b.off, b.length, LOCAL4, LOCAL6, status=b.status)  # current stream
 
+    def _finalize_call(self, b):
+        from rustnetworkstack_amd.batch import tx_fill_chain
+        return lambda: tx_fill_chain(b.arena, b.d_off, b.d_len, b.d_first, status=b.status)  # current stream
+
     def step(self):
         b = self.batches[self.k % len(self.batches)]
         self.used.add(self.k % len(self.batches))
         self.k += 1
-        if self.op == "verify":
+        if self.op == "finalize":
+            self._finalize_call(b)()
+        elif self.op == "verify":
             self._verify_call(b)()
         else:
             b.launcher(complement=True, shape=self.shape, compact=self.compact, packed=self.packed,
@@ -506,7 +549,9 @@ class GpuEngine:
                 b = self.batches[i % len(self.batches)]
                 self.used.add(i % len(self.batches))
                 with torch.cuda.stream(lanes[i % len(lanes)]):
-                    if self.op == "verify":
+                    if self.op == "finalize":
+                        self._finalize_call(b)()
+                    elif self.op == "verify":
                         self._verify_call(b)()
                     else:
                         b.rebind(complement=True, shape=self.shape, compact=self.compact, packed=self.packed,
@@ -575,6 +620,10 @@ class GpuEngine:
 
     def kernel_name(self) -> str:
         from rustnetworkstack_amd import _lib
+        if self.op == "finalize":
+            return ("csum_txrows_kernel FIN (rns_tx_fill_chain_dev: one wave per 64 chains streams the packed "
+                    "payloads as 1 KiB rows, each owner parses its head, and the wave writes its back-to-back heads "
+                    "back as whole chunks from LDS)")
         if self.op == "verify":
             if self.verify_strided:
                 return ("csum_strided_rx_kernel (rns_rx_verify_strided_dev: datagrams in fixed-size slots; a lane "
@@ -706,6 +755,61 @@ def cpu_baseline(engine: GpuEngine, seconds: float, sample_min_bytes: int = 512 
     }
 
 
+def finalize_parity(engine: GpuEngine, threads: int = 8) -> dict:
+    """--op finalize: the GPU's finalized heads against the C restatement of the reference's transmit
+    path (oracle_tx_chain_fill: tcp.rs:957-973 + ip.rs:140-160 over [head[20..], payload]) run on a
+    host copy of the same arena.  Both fields count as zero, so finalizing the GPU's output again
+    must reproduce it byte for byte; statuses must agree."""
+    import numpy as np
+
+    from oracle.oracle import get_oracle
+    b = engine.batches[0]
+    lay = b.layout
+    host = b.arena.cpu().numpy()
+    gpu_st = b.status.cpu().numpy()
+    cpu = host.copy()
+    st = get_oracle().tx_chain_fill(cpu, lay.frag_off, lay.frag_len, lay.first, threads=threads)
+    return {"bit_exact": bool(np.array_equal(cpu, host) and np.array_equal(st, gpu_st)),
+            "packets": int(lay.n), "arena": cpu, "layout": lay}
+
+
+def cpu_baseline_finalize(engine: GpuEngine, seconds: float) -> dict:
+    """--op finalize's CPU baseline: oracle_tx_chain_fill (gcc -O3; the reference's per-datagram
+    transmit path: compute_pseudo_header_checksum + compute_buffer_ones_comp over the chain + the
+    IPv4 header's compute_checksum + two set_be16) over rank 0's first batch, on every granted
+    thread and on one; the GPU's heads are checked against it in the same pass."""
+    grant = cpu_grant()
+    par = finalize_parity(engine, threads=grant["threads"])
+    cpu, lay = par.pop("arena"), par.pop("layout")
+    from oracle.oracle import get_oracle
+    orc = get_oracle()
+
+    def rate(threads: int, budget: float):
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            orc.tx_chain_fill(cpu, lay.frag_off, lay.frag_len, lay.first, threads=threads)
+            passes += 1
+            dt = time.perf_counter() - t0
+            if dt >= budget:
+                return lay.payload_bytes * passes / dt / 2 ** 30, passes, dt
+
+    vmt, passes_mt, dt_mt = rate(grant["threads"], max(seconds / 2, 1.0))
+    v1, passes1, dt1 = rate(1, seconds)
+    return {
+        "value": round(vmt, 3), "unit": "GiB/s", "cores": grant["threads"], "kind": "port",
+        "sample": f"rank 0's first {engine.layout.name} chain batch: {lay.n} datagrams, {lay.payload_bytes} B in "
+                  f"{lay.arena_bytes} B of arena (> host L3); {grant['threads']} threads x {passes_mt} passes in "
+                  f"{dt_mt:.1f} s, 1 thread x {passes1} passes in {dt1:.1f} s",
+        "what": "gcc -O3 restatement of the transmit path (oracle/csum_oracle.c oracle_tx_chain_fill: tcp.rs:957-973, "
+                "udp.rs:151-171, icmp.rs:87-112, ip.rs:140-160 over buf.rs's head fragment), not the Rust build; "
+                "datagrams partitioned by index over threads",
+        "value_1_thread": round(v1, 3),
+        "threads_granted": grant["threads"], "host_cpus_visible": grant["visible"],
+        "cgroup_cpu_quota": grant["quota_cpus"],
+        "gpu_sample_bit_exact": par["bit_exact"],
+    }
+
+
 def host_pipeline_rate(engine: GpuEngine) -> dict:
     """PCIe-inclusive rate: the same batch from pinned host memory through
     rns_csum_batch_host (chunked H2D + kernel + D2H of results on 3 streams).
@@ -785,6 +889,22 @@ def load_traffic(path: str, config: str):
     return t
 
 
+def load_traffic_finalize(config: str):
+    """HBM bytes per finalize launch from the PMC passes over the same kernel and layout
+    (profiles/r06_pmc_write_tx_chain.json: FETCH_SIZE (gfx950-corrected) + WRITE_SIZE)."""
+    path = os.path.join(ROOT, "profiles", "r06_pmc_write_tx_chain.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        k = d[config]["per_kernel"]["tx_chain"]
+        v = next(iter(k.values()))
+        return {"hbm_bytes_per_launch": int(v["fetch_bytes_corrected"] + v["write_bytes"]),
+                "source": f"{os.path.relpath(path, ROOT)} (session {d.get('session')}: rocprofv3 --pmc FETCH_SIZE / "
+                          "WRITE_SIZE / TCC_EA0_WRREQ, separate passes)"}
+    except (OSError, KeyError, ValueError, StopIteration):
+        return None
+
+
 def launch_ranks(args, argv) -> int:
     """`--gpus N` (N > 1) without a torch.distributed launcher: start N ranks of this
     same script under `torch.distributed.run` as a CHILD process (never an exec: no
@@ -826,8 +946,11 @@ def main(argv=None):
     shape = tuple(int(x) for x in args.shape.split(",")) if args.shape else None
     strong = args.scaling == "strong" or (args.scaling == "auto" and args.config == "c5_imix")
     verify = args.op == "verify"
+    finalize = args.op == "finalize"
     if verify:
         args.no_cpu_baseline = args.no_host_pipeline = True  # the headline's CPU legs; not this mode's
+    if finalize:
+        args.no_host_pipeline = args.no_gather = True  # nothing crosses ranks; the pipeline is TxChainPipeline
     if args.shard_rw is not None and dist.world > 1:
         raise SystemExit("--shard r/N is a one-process measurement of one rank's shard (use --scaling strong at N>1)")
     if args.shard_rw is not None:
@@ -866,17 +989,19 @@ def main(argv=None):
         ri = timed_loop(engine, _NoDist(), args.steps, 0, graph=engine.capture(args.steps, 1))
         isolated = ri["kernel_ms"] * 1e3
     per = engine.per_launch_us(args.median_launches) if args.median_launches > 0 else []
-    # payload read + the result written: u16 sum (csum) or u8 status (verify)
-    algo_bytes = engine.payload_bytes + (1 if verify else 2) * engine.n
+    # payload read + the result written: u16 sum (csum), u8 status (verify), or the two 2-byte fields
+    # and the u8 status (finalize)
+    algo_bytes = engine.payload_bytes + (5 if finalize else 1 if verify else 2) * engine.n
     # descriptor bytes a launch reads (seeds included): packed 2 B length + 8 B per 64 packets
-    desc_bytes = (engine.n * (2 + (0 if verify else 2)) + 8 * ((engine.n + 63) // 64) if engine.packed
+    desc_bytes = (12 * engine.batches[0].n_frags + 4 * (engine.n + 1) if finalize  # u64 off + u32 len, u32 first
+                  else engine.n * (2 + (0 if verify else 2)) + 8 * ((engine.n + 63) // 64) if engine.packed
                   else 2 * engine.n if getattr(engine, "strided", False)  # the seeds (verify: the u16 lengths)
                   else engine.n * ((4 if engine.compact else 8) + 4 + (0 if verify else 2)))
     kernel_us = kernel_ms * 1e3
     achieved = algo_bytes / (kernel_us * 1e-6) / 1e9
-    traffic = load_traffic(args.traffic_json, args.config)
+    traffic = load_traffic_finalize(args.config) if finalize else load_traffic(args.traffic_json, args.config)
     line = {
-        "metric": METRIC_VERIFY if verify else METRIC,
+        "metric": METRIC_FINALIZE if finalize else METRIC_VERIFY if verify else METRIC,
         "value": round(value, 2),
         "unit": "GiB/s",
         "n_gpus": dist.world,
@@ -891,11 +1016,18 @@ def main(argv=None):
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": ("synthetic: IPv4/TCP datagrams to 10.0.0.2 (splitmix64 payload, seed 0x5EEDC0DE + per-rank "
+        "data": ("synthetic: IPv4/TCP datagrams from 10.0.0.2 to 10.0.0.1 as NetBuffer chains (IPv4 header written, "
+                 "TCP header and payload splitmix64 bytes, seed 0x5EEDC0DE + per-rank offset; checksum fields hold "
+                 "whatever is there and count as zero)" if finalize else
+                 "synthetic: IPv4/TCP datagrams to 10.0.0.2 (splitmix64 payload, seed 0x5EEDC0DE + per-rank "
                  "offset; checksums filled by rns_tx_fill_dev; every 1009th datagram corrupted)" if verify else
                  "synthetic: splitmix64 packet bytes (seed 0x5EEDC0DE + per-rank offset), per-packet u16 seeds"),
         "config": {
-            "workload": (f"{args.config} verify: {engine.n} IPv4/TCP datagrams x "
+            "workload": (f"{args.config} finalize: {engine.n} IPv4/TCP datagrams x "
+                         f"{engine.payload_bytes // max(engine.n, 1)} B per GPU as [40 B head fragment, payload] chains "
+                         "(heads back to back in a header region, payloads packed at 16 B), IPv4 header + TCP "
+                         "checksums computed and stored into the heads, u8 status out" if finalize else
+                         f"{args.config} verify: {engine.n} IPv4/TCP datagrams x "
                          f"{engine.payload_bytes // max(engine.n, 1)} B per GPU, 16 B-aligned arena in HBM, "
                          "IPv4 header + TCP checksum checked, u8 status out" if verify else
                          f"{args.config}: {engine.n} packets x {engine.payload_bytes // max(engine.n, 1)} B per GPU, "
@@ -905,7 +1037,9 @@ def main(argv=None):
             "batch": "one batch sharded by packet index across ranks" if strong else "a full batch per rank",
             "parallelism": f"packet shards x{dist.world}, no data-path collective in `value`",
             "kernel_shape": list(shape) if shape else "auto",
-            "descriptors": ({"64": "u64 offset + u32 length per datagram (rns_rx_verify_dev)",
+            "descriptors": ({"chain": "u64 offset + u32 length per fragment, u32 first fragment per datagram "
+                                      "(rns_tx_fill_chain_dev)"} if finalize else
+                            {"64": "u64 offset + u32 length per datagram (rns_rx_verify_dev)",
                              "packed": "packed: u16 length per datagram, u64 offset per 64 datagrams "
                                        "(rns_rx_verify_packed_dev)",
                              "strided": "strided: u16 length per datagram, offsets implied by the slot stride "
@@ -1006,7 +1140,23 @@ def main(argv=None):
             "value_gather_overlap": "eager; step i's all-gather on a side stream under step i+1's kernel "
                                     "(OverlappedGather, DESIGN §6)",
             "gather_ms": "eager; the all-gather alone, per step"}
-    if dist.world > 1 and not verify:
+    if finalize:
+        # every rank: its first batch's heads against the CPU restatement; rank 0 then times it
+        par = finalize_parity(engine, threads=max(1, min(8, cpu_grant()["threads"])))
+        par.pop("arena", None)
+        par.pop("layout", None)
+        ranks_exact = int(dist.sum(1.0 if par["bit_exact"] else 0.0))
+        line["parity"] = {"ranks_bit_exact": ranks_exact, "ranks": dist.world,
+                          "packets_checked": int(dist.sum(float(par["packets"]))),
+                          "bit_exact_all_ranks": ranks_exact == dist.world,
+                          "how": "every rank: every byte of its first batch's arena and every status after the timed "
+                                 "legs vs oracle_tx_chain_fill run on a host copy (both fields count as zero, so the "
+                                 "CPU must reproduce the GPU's heads); the counts are all-reduced"}
+        dist.barrier()
+        if dist.rank == 0 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline_finalize(engine, args.cpu_seconds)
+        dist.barrier()
+    if dist.world > 1 and not verify and not finalize:
         # after every rank's GPU legs: each rank checks its own results; rank 0 times the CPU
         # baseline on its own batch while the others wait (benches/util_bench.rs:20-45 beside
         # the N-GPU figure, on the same box's host cores, in the same run)
@@ -1024,7 +1174,7 @@ def main(argv=None):
                           "bit_exact_all_ranks": ranks_exact == dist.world,
                           "how": "every rank: every packet of its first batch vs the oracle (util.rs:88-106 "
                                  "restated), after the timed legs; the counts are all-reduced"}
-    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline and not finalize:
         line["cpu_baseline"] = cpu_baseline(engine, args.cpu_seconds)
     if dist.rank == 0 and dist.world == 1 and not args.no_host_pipeline:
         line["host_inclusive"] = host_pipeline_rate(engine)

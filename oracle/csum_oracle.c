@@ -202,3 +202,124 @@ void oracle_chain_batch(const uint8_t *arena, const uint64_t *frag_off, const ui
         out[i] = (uint16_t)(complement ? (0xffff ^ (uint32_t)sum) : (uint32_t)sum);
     }
 }
+
+/*
+ * Transmit finalize of NetBuffer chains (oracle.tx_chain_fill_ref in C; bench.py --op finalize's
+ * CPU baseline).  Datagram i = fragments [first[i], first[i+1]): fragment first[i] is the head
+ * alloc_header built (buf.rs:262-291: the IP header, then the L4 header), the rest the payload.
+ * tcp_output / udp_output / icmp_output_* (tcp.rs:957-973, udp.rs:151-171, icmp.rs:87-112):
+ * pseudo-header from the head's addresses and the chain's length, compute_buffer_ones_comp over
+ * [head[hdr..], payload...] with the field zeroed, set_be16 of 0xffff ^ it; ip_output_v4
+ * (ip.rs:140-160): compute_checksum(head[..IHL*4]) with [10..12] zeroed.  status[i] = TX bits
+ * (1 IP filled, 2 L4 filled, 0x80 malformed: no fragments, a fragment outside the arena, a head
+ * that does not hold the IP header, a bad version — left unchanged).  Empty pieces add nothing.
+ */
+static uint8_t tx_chain_fill_one(uint8_t *arena, uint64_t arena_bytes, const uint64_t *fo, const uint32_t *fl,
+                                 uint32_t f0, uint32_t f1)
+{
+    if (f1 <= f0)
+        return 0x80;
+    uint64_t L = 0;
+    for (uint32_t f = f0; f < f1; f++) {
+        if (fo[f] > arena_bytes || fl[f] > arena_bytes - fo[f])
+            return 0x80;
+        L += fl[f];
+    }
+    uint8_t *h = arena + fo[f0];
+    const uint32_t hl = fl[f0];
+    if (hl == 0)
+        return 0x80;
+    const uint32_t version = h[0] >> 4;
+    uint32_t hdr, proto;
+    const uint8_t *src, *dst;
+    size_t alen;
+    if (version == 4) {
+        hdr = (h[0] & 15u) * 4u;
+        if (hdr < 20 || hdr > hl)
+            return 0x80;
+        proto = h[9]; src = h + 12; dst = h + 16; alen = 4;
+    } else if (version == 6) {
+        hdr = 40;
+        if (hl < 40)
+            return 0x80;
+        proto = h[6]; src = h + 8; dst = h + 24; alen = 16;
+    } else {
+        return 0x80;
+    }
+    const uint64_t seg = L - hdr;
+    int field = -1;
+    int32_t seed = 0;
+    if (proto == 6 || proto == 17) {
+        field = proto == 6 ? 16 : 6;
+        seed = oracle_compute_pseudo_header_checksum(src, alen, dst, alen, seg & 0xffff, (uint8_t)proto);
+    } else if (proto == 1 && version == 4) {
+        field = 2;
+    } else if (proto == 58 && version == 6) {
+        field = 2;
+        seed = oracle_compute_pseudo_header_checksum(src, alen, dst, alen, seg, 58);
+    }
+    uint8_t st = 0;
+    if (field >= 0 && seg >= (uint64_t)field + 2 && hdr + (uint32_t)field + 2 <= hl) {
+        uint8_t *fp = h + hdr + field;
+        fp[0] = fp[1] = 0;
+        int32_t acc = seed;
+        if (hl > hdr)
+            acc = oracle_compute_ones_comp((uint16_t)acc, h + hdr, hl - hdr);
+        for (uint32_t f = f0 + 1; f < f1; f++)
+            if (fl[f])
+                acc = oracle_compute_ones_comp((uint16_t)acc, arena + fo[f], fl[f]);
+        set_be16(fp, (uint16_t)(0xffff ^ (uint32_t)acc));
+        st |= 2;
+    }
+    if (version == 4) {
+        h[10] = h[11] = 0;
+        set_be16(h + 10, (uint16_t)oracle_compute_checksum(h, hdr));
+        st |= 1;
+    }
+    return st;
+}
+
+void oracle_tx_chain_fill(uint8_t *arena, uint64_t arena_bytes, const uint64_t *frag_off, const uint32_t *frag_len,
+                          const uint32_t *first, uint32_t n_frags, size_t n, uint8_t *status)
+{
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t f0 = first[i], f1 = first[i + 1];
+        status[i] = (f0 <= f1 && f1 <= n_frags) ? tx_chain_fill_one(arena, arena_bytes, frag_off, frag_len, f0, f1)
+                                                : 0x80;
+    }
+}
+
+struct txc_job {
+    uint8_t *arena; uint64_t arena_bytes; const uint64_t *fo; const uint32_t *fl; const uint32_t *first;
+    uint32_t n_frags; uint8_t *status; size_t lo, hi;
+};
+
+static void *txc_worker(void *arg)
+{
+    struct txc_job *j = (struct txc_job *)arg;
+    oracle_tx_chain_fill(j->arena, j->arena_bytes, j->fo, j->fl, j->first + j->lo, j->n_frags, j->hi - j->lo,
+                         j->status + j->lo);
+    return NULL;
+}
+
+/* The same partitioned by datagram index over host threads (datagrams must not share heads). */
+int oracle_tx_chain_fill_mt(uint8_t *arena, uint64_t arena_bytes, const uint64_t *frag_off, const uint32_t *frag_len,
+                            const uint32_t *first, uint32_t n_frags, size_t n, uint8_t *status, int nthreads)
+{
+    pthread_t tid[256];
+    struct txc_job job[256];
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    for (int t = 0; t < nthreads; t++) {
+        job[t] = (struct txc_job){arena, arena_bytes, frag_off, frag_len, first, n_frags, status,
+                                  n * t / nthreads, n * (t + 1) / nthreads};
+        if (pthread_create(&tid[t], NULL, txc_worker, &job[t]) != 0) {
+            for (int u = 0; u < t; u++)
+                pthread_join(tid[u], NULL);
+            return -1;
+        }
+    }
+    for (int t = 0; t < nthreads; t++)
+        pthread_join(tid[t], NULL);
+    return 0;
+}

@@ -339,6 +339,12 @@ class Oracle:
         L.oracle_batch_mt.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
         L.oracle_chain_batch.restype = None
         L.oracle_chain_batch.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_size_t, ctypes.c_int]
+        L.oracle_tx_chain_fill.restype = None
+        L.oracle_tx_chain_fill.argtypes = [ctypes.c_void_p, ctypes.c_uint64] + [ctypes.c_void_p] * 3 + [
+            ctypes.c_uint32, ctypes.c_size_t, ctypes.c_void_p]
+        L.oracle_tx_chain_fill_mt.restype = ctypes.c_int
+        L.oracle_tx_chain_fill_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint64] + [ctypes.c_void_p] * 3 + [
+            ctypes.c_uint32, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int]
         L.oracle_time_ones_comp.restype = ctypes.c_double
         L.oracle_time_ones_comp.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]
 
@@ -413,6 +419,25 @@ class Oracle:
         self.lib.oracle_chain_batch(arena.ctypes.data, frag_off.ctypes.data, frag_len.ctypes.data, first.ctypes.data,
                                     sp, out.ctypes.data, n, int(complement))
         return out
+
+    def tx_chain_fill(self, arena: np.ndarray, frag_off: np.ndarray, frag_len: np.ndarray, first: np.ndarray,
+                      threads: int = 1) -> np.ndarray:
+        """tx_chain_fill_ref for a batch of chains, IN PLACE on ``arena`` (a writable uint8 array):
+        the heads get their checksums; returns the status per datagram."""
+        if arena.dtype != np.uint8 or not arena.flags.c_contiguous or not arena.flags.writeable:
+            raise ValueError("arena must be a writable contiguous uint8 array (filled in place)")
+        frag_off = np.ascontiguousarray(frag_off, dtype=np.uint64)
+        frag_len = np.ascontiguousarray(frag_len, dtype=np.uint32)
+        first = np.ascontiguousarray(first, dtype=np.uint32)
+        n = first.shape[0] - 1
+        st = np.empty(max(n, 0), dtype=np.uint8)
+        args = (arena.ctypes.data, arena.shape[0], frag_off.ctypes.data, frag_len.ctypes.data, first.ctypes.data,
+                frag_off.shape[0], n, st.ctypes.data)
+        if threads <= 1:
+            self.lib.oracle_tx_chain_fill(*args)
+        elif self.lib.oracle_tx_chain_fill_mt(*args, int(threads)) != 0:
+            raise RuntimeError("oracle_tx_chain_fill_mt: thread creation failed")
+        return st
 
     def time_ones_comp(self, data: bytes, iters: int) -> float:
         """ns per compute_ones_comp(0, data) call (benches/util_bench.rs:20-45 equivalent)."""

@@ -361,3 +361,46 @@ def tx_chain_layout(name: str, n: int | None = None, head: int = 20, frag: int =
     return TxChainLayout(name=name, frag_off=off.astype(np.uint64), frag_len=ln.astype(np.uint32),
                          first=first.astype(np.uint32), seed=lay.seed, field=field, head=head,
                          arena_bytes=arena_bytes, data_seed=lay.data_seed, payload_bytes=lay.payload_bytes)
+
+
+class TxChainBatch:
+    """A transmit batch as NetBuffer chains in HBM (bench.py --op finalize): the chains of
+    tx_chain_layout(config, head=40) — 40-byte head fragments (an IPv4 header from LOCAL4 to
+    REMOTE4, then the TCP header alloc_header left: splitmix64 bytes, the checksum fields counting
+    as zero) back to back in a header region, the payloads packed at 16-byte starts — with the
+    fragment descriptors and a status array on the device.  A finalize of it stores the two
+    checksums into every head (rns_tx_fill_chain_dev); finalizing again stores the same bytes."""
+
+    HEAD = 40  # IPv4 header + TCP header
+
+    def __init__(self, config: str, device, data_seed: int = DATA_SEED, frag: int = 0,
+                 shard: tuple[int, int] = (0, 1)):
+        import torch
+
+        from .batch import fill_splitmix64
+        lay = tx_chain_layout(config, head=self.HEAD, frag=frag, data_seed=data_seed, shard=shard)
+        self.layout = lay
+        self.device = device
+        n = lay.n
+        first = lay.first.astype(np.int64)
+        self.length = (np.add.reduceat(lay.frag_len.astype(np.int64), first[:-1]) if n
+                       else np.zeros(0, dtype=np.int64))
+        if n and int(self.length.min()) < MIN_DATAGRAM:
+            raise ValueError(f"finalize batches need datagrams of at least {MIN_DATAGRAM} B")
+        self.hoff = lay.frag_off[first[:-1]].astype(np.int64) if n else np.zeros(0, dtype=np.int64)
+        self.arena = torch.empty(lay.arena_bytes + 64, dtype=torch.uint8, device=device)
+        fill_splitmix64(self.arena, lay.data_seed)
+        hdr = torch.from_numpy(ipv4_tcp_headers(self.length, LOCAL4, REMOTE4)).to(device)
+        d_hoff = torch.from_numpy(self.hoff).to(device)
+        step = 1 << 20  # datagrams per scatter (bounds the index tensor)
+        for i in range(0, n, step):
+            idx = d_hoff[i:i + step].view(-1, 1) + torch.arange(20, device=device)
+            self.arena[idx.flatten()] = hdr[i:i + step].flatten()
+        self.d_off = torch.from_numpy(lay.frag_off.view(np.int64)).to(device)
+        self.d_len = torch.from_numpy(lay.frag_len.view(np.int32)).to(device)
+        self.d_first = torch.from_numpy(lay.first.view(np.int32)).to(device)
+        self.status = torch.empty(n, dtype=torch.uint8, device=device)
+
+    @property
+    def n_frags(self) -> int:
+        return int(self.layout.frag_off.shape[0])

@@ -34,3 +34,19 @@ def test_bench_verify_descriptor_form_matches():
                        "--ramp-s", "0", "--traffic-json", "/nonexistent/{config}.json"])
     assert line["roofline"]["kernel"].startswith("csum_mixed_kernel<RX>")
     assert line["verify"]["rejected_total"] == line["verify"]["rejected_expected"] > 0
+
+
+@pytest.mark.parametrize("config", ["c2_64B", "c3_1500B"])
+def test_bench_finalize_line(config):
+    """bench.py --op finalize (SURVEY §8(f) row 2 through the bench harness): one
+    rns_tx_fill_chain_dev launch per step over NetBuffer chains; after the timed steps the GPU's
+    heads and statuses equal the C restatement of the transmit path run on a host copy, and the
+    line carries the roofline and the CPU baseline of that restatement."""
+    line = bench.main(["--config", config, "--op", "finalize", "--steps", "6", "--warmup", "1", "--ramp-s", "0",
+                       "--cpu-seconds", "1"])
+    assert line["metric"] == bench.METRIC_FINALIZE
+    assert line["parity"]["bit_exact_all_ranks"] and line["parity"]["packets_checked"] > 0
+    assert line["roofline"]["kernel"].startswith("csum_txrows_kernel FIN")
+    assert 0 < line["roofline"]["frac"] < 1.0
+    cb = line["cpu_baseline"]
+    assert cb["gpu_sample_bit_exact"] and cb["value"] > 0 and cb["kind"] == "port"

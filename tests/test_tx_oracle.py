@@ -136,3 +136,49 @@ def test_chain_fill_rejects_and_partial_fills():
     assert st == 0 and head == v6[:40]
     head, st = O.tx_chain_fill_ref([pkt[:38], b"", pkt[38:]])                          # empty piece: nothing
     assert st == O.TX_IP_FILLED | O.TX_L4_FILLED and head == O.tx_fill_ref(pkt)[0][:38]
+
+
+def test_chain_fill_c_restatement_equals_python(oracle):
+    """oracle_tx_chain_fill (C: bench.py --op finalize's CPU baseline) == tx_chain_fill_ref on
+    random chains of every datagram kind: heads cut anywhere, odd pieces, empty pieces, no
+    fragments, fragments outside the arena; 1 thread and 4."""
+    import numpy as np
+    from test_gpu_tx import outgoing
+    pkts = outgoing(1500, 0xC0C0)
+    w = O.splitmix64_words(0xC0C1, 4 * len(pkts))
+    arena = bytearray()
+    off, ln, first, chains = [], [], [0], []
+    for i, p in enumerate(pkts):
+        if i % 97 == 5:
+            first.append(len(off))
+            chains.append(None)
+            continue
+        cuts = sorted({int(w[4 * i + k]) % (len(p) + 1) for k in range(1 + int(w[4 * i + 3] % np.uint64(3)))})
+        hl = min(len(p), 20 + int(w[4 * i] % np.uint64(50))) if i % 3 else cuts[0]
+        b = [0, hl] + [c for c in cuts if c > hl] + [len(p)]
+        frags = [p[b[k]:b[k + 1]] for k in range(len(b) - 1)]
+        if not frags[-1] and len(frags) > 1:
+            frags = frags[:-1]
+        for f in frags:
+            arena += bytes(int(w[4 * i + 1] % np.uint64(5)))
+            off.append(len(arena))
+            ln.append(len(f))
+            arena += f
+        first.append(len(off))
+        chains.append(frags)
+    off.append(1 << 40)                       # a chain with a fragment outside the arena
+    ln.append(4)
+    first.append(len(off))
+    chains.append(None)
+    arena_np = np.frombuffer(bytes(arena), dtype=np.uint8)
+    for threads in (1, 4):
+        a = arena_np.copy()
+        st = oracle.tx_chain_fill(a, np.array(off, np.uint64), np.array(ln, np.uint32), np.array(first, np.uint32),
+                                  threads=threads)
+        for i, frags in enumerate(chains):
+            if frags is None:
+                assert st[i] == O.TX_MALFORMED
+                continue
+            h, s = O.tx_chain_fill_ref(frags)
+            o = off[first[i]]
+            assert st[i] == s and bytes(a[o:o + len(h)]) == h, i
