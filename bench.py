@@ -955,6 +955,10 @@ def main(argv=None):
         raise SystemExit("--shard r/N is a one-process measurement of one rank's shard (use --scaling strong at N>1)")
     if args.shard_rw is not None:
         strong = True
+    if args.graph_streams <= 0 and args.op == "finalize":
+        # two finalizes at once slow each other (c3: 285.9 us per step over 2 streams against 277.6
+        # one after another, r06o): the transmit kernels run on one stream
+        args.graph_streams = 1
     if args.graph_streams <= 0:
         from rustnetworkstack_amd.workloads import make_layout
         from rustnetworkstack_amd.workloads import CONFIGS
