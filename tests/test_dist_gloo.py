@@ -271,6 +271,101 @@ def test_two_rank_gloo_verify_allreduce(tmp_path, config, n):
     assert line["cpu_baseline"] is None
 
 
+FINALIZE_WORKER = r"""
+import json, os, sys, time
+sys.path.insert(0, {root!r})
+import numpy as np
+import torch
+import bench
+from oracle import oracle as O
+from rustnetworkstack_amd import workloads as W
+
+N = {n}
+
+class _Batch:
+    pass
+
+class CpuFinalizeEngine(bench.GpuEngine):
+    # Stand-in for bench.GpuEngine in finalize mode: the same NetBuffer chains (40-byte IPv4+TCP
+    # heads back to back, payloads packed) in a host arena, each step = the oracle's transmit
+    # restatement over them; with PLANT, rank 1 leaves one wrong field (parity is per rank).
+    def __init__(self, config, rank, local_rank, shape=None, steps=0, world=1, strong=False, compact="64",
+                 op="csum", min_batches=1, shard=None):
+        assert op == "finalize"
+        self.torch, self.op = torch, op
+        self.device = torch.device("cpu")
+        lay = W.tx_chain_layout(config, n=N, head=40, data_seed=0x5EEDC0DE + 0x1000 * rank,
+                                shard=(rank, world) if strong else (0, 1))
+        self.layout = lay
+        first = lay.first.astype(np.int64)
+        length = np.add.reduceat(lay.frag_len.astype(np.int64), first[:-1])
+        arena = O.splitmix64_bytes(lay.data_seed, lay.arena_bytes + 64)
+        hoff = lay.frag_off[first[:-1]].astype(np.int64)
+        hdr = W.ipv4_tcp_headers(length, W.LOCAL4, W.REMOTE4)
+        for i in range(lay.n):
+            arena[hoff[i]:hoff[i] + 20] = hdr[i]
+        b = _Batch()
+        b.layout, b.arena = lay, torch.from_numpy(arena)
+        b.status = torch.zeros(lay.n, dtype=torch.uint8)
+        b.n_frags = int(lay.frag_off.shape[0])
+        self.batches = [b]
+        self.last = b
+        self.rank = rank
+        self.compact, self.shape, self.k, self.timed = False, None, 0, 0
+        self.packed, self.strided, self.form, self.used = False, False, "chain", {{0}}
+        self.gatherer = self.reducer = None
+    def step(self):
+        b = self.batches[0]
+        st = O.get_oracle().tx_chain_fill(b.arena.numpy(), self.layout.frag_off, self.layout.frag_len,
+                                          self.layout.first)
+        b.status.copy_(torch.from_numpy(st))
+        if self.rank == 1 and {plant}:
+            b.arena[int(self.layout.frag_off[0]) + 36] ^= 1      # a wrong TCP checksum on rank 1
+    def sync(self):
+        pass
+    def begin_timing(self):
+        self.t0 = time.perf_counter()
+    def end_timing(self, steps):
+        self.ms = 1e3 * (time.perf_counter() - self.t0) / steps
+        self.timed = steps
+    def kernel_ms(self):
+        return self.ms
+    def kernel_name(self):
+        return "cpu stand-in"
+
+bench.GpuEngine = CpuFinalizeEngine
+line = bench.main(["--gpus", "2", "--config", {config!r}, "--op", "finalize", "--steps", "2", "--warmup", "1",
+                   "--cpu-seconds", "0.2", "--ramp-s", "0"])
+rank = int(os.environ["RANK"])
+with open(os.path.join({outdir!r}, f"rank{{rank}}.json"), "w") as f:
+    json.dump({{"rank": rank, "line": line}}, f)
+"""
+
+
+@pytest.mark.parametrize("plant", [False, True])
+def test_two_rank_gloo_finalize_parity(tmp_path, plant):
+    """Finalize mode at N=2: no collective on the data path (no gather legs), every rank checks its
+    own batch against the transmit restatement and the counts are all-reduced — a wrong field on
+    one rank shows as 1 of 2 ranks bit-exact; rank 0 alone times the CPU baseline."""
+    script = tmp_path / "worker.py"
+    script.write_text(FINALIZE_WORKER.format(root=ROOT, n=3000, config="c3_1500B", outdir=str(tmp_path),
+                                             plant=plant))
+    env = dict(os.environ, OMP_NUM_THREADS="1", RNS_BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(script)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    printed = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(printed) == 1
+    line = printed[0]
+    assert line["metric"] == __import__("bench").METRIC_FINALIZE
+    assert line["parity"]["ranks"] == 2 and line["parity"]["packets_checked"] == 6000
+    assert line["parity"]["ranks_bit_exact"] == (1 if plant else 2)
+    assert "value_gather" not in line and "allreduce" not in line
+    assert line["cpu_baseline"]["kind"] == "port" and line["cpu_baseline"]["value"] > 0
+    assert line["cpu_baseline"]["gpu_sample_bit_exact"] is True          # rank 0's batch is intact
+
+
 def test_gpus_disagreeing_with_world_size_fails(tmp_path):
     """--gpus 2 under a launcher that says WORLD_SIZE=1 must exit non-zero, before any
     engine is built (no silent one-rank line for a two-GPU request)."""
