@@ -981,6 +981,9 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : RNS_ROWS_TX_OCC) void csum_rows_t
 #define RNS_TXROWS_OCC 5  // (zero scratch at 86-89 VGPRs; 6 spills 32-116 B/lane)
 #endif
 constexpr uint32_t kTxHeadMax = 64;  // (head start & 15) + head length: at most 4 chunks (5 for FIN)
+#ifndef RNS_TXFIN_RUN_AUX  // cache-policy bits of the run write-back's chunk stores: nontemporal (c3 277.3 ->
+#define RNS_TXFIN_RUN_AUX kNtAux  // 270.1 us cold, IMIX 626.4 -> 624.7; plain stores 282.2 / 634.6: r06t)
+#endif
 #ifndef RNS_TXFIN_RUNWRITE  // FIN: write a wave's back-to-back heads back as whole chunks
 #define RNS_TXFIN_RUNWRITE 1  // (IMIX 652.1-652.2 -> 632.5 us, c3 257.3 -> 256.0 against two 2-byte
 #endif                        //  stores per head: session r06h, txops / txops_rw)
@@ -1284,7 +1287,7 @@ __global__ __launch_bounds__(64, RNS_TXROWS_OCC) void csum_txrows_kernel(const C
                 const uint4 v = run_lds[(c - b0) >> 4];
                 if constexpr (BUF) {
                     const u32x4 y = {v.x, v.y, v.z, v.w};
-                    __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, static_cast<uint32_t>(c), 0, RNS_STREAM_OUT_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, static_cast<uint32_t>(c), 0, RNS_TXFIN_RUN_AUX);
                 } else {
                     *reinterpret_cast<uint4 *>(w8 + c) = v;
                 }
