@@ -637,6 +637,9 @@ __global__ __launch_bounds__(64, kStridedRxOcc) void csum_strided_rx_kernel(cons
 #ifndef RNS_ROWS_TX_OCC  // waves/SIMD bound of the transmit form
 #define RNS_ROWS_TX_OCC 6
 #endif
+#ifndef RNS_ROWS_TX_FIELD_AUX  // cache-policy bits of the packed finalize's field stores
+#define RNS_ROWS_TX_FIELD_AUX 0
+#endif
 constexpr uint32_t kNoField = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t bswap16_u32(uint32_t x) { return ((x & 0xff) << 8) | (x >> 8); }
@@ -939,7 +942,7 @@ __global__ __launch_bounds__(64, D >= 16 ? 4 : RNS_ROWS_TX_OCC) void csum_rows_t
 #pragma unroll
     for (int k = 0; k < 2; ++k)
         if (fld[k] != kNoField)
-            store_field<BUF>(a, rsrc, start + fld[k], val[k]);
+            store_field<BUF, RNS_ROWS_TX_FIELD_AUX>(a, rsrc, start + fld[k], val[k]);
     if (live && a.status)
         a.status[p] = st;
 }
