@@ -844,8 +844,11 @@ const char *rns_build_info(void)
     return "rns_checksum abi=1 offload-arch=gfx950 kernels=csum_rows_kernel (packed form: 1 KiB rows per 64-packet "
            "region, owners capture two region prefixes and sum their own end chunk; fill mode), csum_rows_rx_kernel "
            "(packed receive verify: the rows plus each owner's header chunks loaded a group ahead), csum_stream_kernel "
-           "(receive verify of ACK-sized arenas: owners load their datagrams whole), csum_txrows_kernel (transmit-shaped "
-           "chains: packed payload rows + owner-loaded head fragments; head-fragment fill), csum_strided_tiny_kernel "
+           "(receive verify of ACK-sized arenas: owners load their datagrams whole), csum_strided_rx_kernel (receive "
+           "verify of fixed-size slots: quad-coalesced rows), csum_rows_tx_kernel (packed transmit finalize through the "
+           "rows), csum_txrows_kernel (transmit-shaped chains: packed payload rows + owner-loaded head fragments; "
+           "head-fragment fill; whole finalize of NetBuffer chains with the heads written back from LDS), "
+           "csum_strided_tiny_kernel "
            "(fixed-size packets <= 64 B at a fixed stride), csum_mixed_kernel (per-wave size-class sort; verify / fill / "
            "transmit-finalize stash modes), csum_rounds_kernel, csum_batch_kernel, csum_chain_kernel (one pass, "
            "per-fragment fold; head-fragment fill) (v_sad_u16 LE sums, v_dot4 BE sums past 128 KiB, wave64, DPP "
